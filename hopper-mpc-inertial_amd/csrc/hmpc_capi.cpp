@@ -1,0 +1,259 @@
+// hmpc_capi.cpp -- the C ABI declared in include/hmpc.h.
+//
+// A context is the device-side counterpart of one reference ``Mpc`` object
+// (src/mpc_cvx_euler_3f.py:12-39): it holds the constants and, for the
+// host-pointer entry points, staging buffers on its device.  Nothing here
+// computes on the CPU: every solve is a kernel launch.
+#include <hip/hip_runtime.h>
+
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <string>
+
+#include "../../include/hmpc.h"
+#include "hmpc_internal.h"
+
+struct hmpc_ctx {
+  int variant;
+  int N;
+  int device;
+  double t, m, g, mu;
+  double Jinv[9];
+  double rh[3];
+  int uref_mode;
+  std::string err;
+  // staging buffers (host API) and mpcontrol scratch
+  void* dbuf = nullptr;
+  size_t dbuf_bytes = 0;
+  int32_t* scratch_i32 = nullptr;
+  int64_t scratch_n = 0;
+  hipStream_t own_stream = nullptr;
+};
+
+namespace {
+
+int fail_hip(hmpc_ctx* c, hipError_t e, const char* where) {
+  if (c) c->err = std::string(where) + ": " + hipGetErrorString(e);
+  return HMPC_ERR_HIP;
+}
+
+#define HMPC_HIP(ctx, call)                                   \
+  do {                                                        \
+    hipError_t e_ = (call);                                   \
+    if (e_ != hipSuccess) return fail_hip((ctx), e_, #call);  \
+  } while (0)
+
+hmpc::SolveArgs make_args(hmpc_ctx* c, int64_t B, const double* x_in, const double* x_lin,
+                          const double* x_ref, const double* pf, const double* C,
+                          const double* mu, double* u, double* x, double* obj, int32_t* status,
+                          int32_t* iters, int shift_mode) {
+  hmpc::SolveArgs a;
+  a.x_in = x_in; a.x_lin = x_lin; a.x_ref = x_ref; a.pf = pf; a.C = C; a.mu = mu;
+  a.u = u; a.x = x; a.obj = obj; a.status = status; a.iters = iters;
+  a.B = B;
+  a.dt = c->t; a.m = c->m; a.g = c->g; a.mu_default = c->mu;
+  memcpy(a.Jinv, c->Jinv, sizeof(a.Jinv));
+  memcpy(a.rh, c->rh, sizeof(a.rh));
+  a.uref_aliased = c->uref_mode == HMPC_UREF_ALIASED ? 1 : 0;
+  a.shift_mode = shift_mode;
+  return a;
+}
+
+__global__ void combine_status(int64_t B, const int32_t* s1, const int32_t* i1, int32_t* s2,
+                               int32_t* i2) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B) return;
+  if (s1[i] > s2[i]) s2[i] = s1[i];
+  if (i2) i2[i] += i1[i];
+}
+
+int check_solve_args(hmpc_ctx* c, int64_t B, const void* x_in, const void* x_lin,
+                     const void* x_ref, const void* pf, const void* C, const void* u,
+                     const void* status) {
+  if (!c) return HMPC_ERR_ARG;
+  if (B < 0) { c->err = "B < 0"; return HMPC_ERR_ARG; }
+  if (B == 0) return HMPC_OK;
+  if (B > 0x7fffffffLL) { c->err = "B exceeds the grid limit"; return HMPC_ERR_ARG; }
+  if (!x_in || !x_lin || !x_ref || !pf || !C || !u || !status) {
+    c->err = "null input/output pointer";
+    return HMPC_ERR_ARG;
+  }
+  return HMPC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int hmpc_version(void) { return 10000; }
+
+int hmpc_supported_horizons(int variant, int* Ns, int cap) {
+  return hmpc::supported_horizons(variant, Ns, cap);
+}
+
+int hmpc_create(hmpc_ctx** out, int variant, int N, double t, double m, double g, double mu,
+                const double* Jinv, const double* rh, int uref_mode, int device) {
+  if (!out || !Jinv || !rh) return HMPC_ERR_ARG;
+  *out = nullptr;
+  if (variant != HMPC_VARIANT_3F && variant != HMPC_VARIANT_2F) return HMPC_ERR_ARG;
+  if (uref_mode != HMPC_UREF_ALIASED && uref_mode != HMPC_UREF_PER_STAGE) return HMPC_ERR_ARG;
+  if (!(t > 0.0) || !(m > 0.0) || N <= 0) return HMPC_ERR_ARG;
+  if (!hmpc::horizon_supported(variant, N)) return HMPC_ERR_UNSUPPORTED;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return HMPC_ERR_HIP;
+  hmpc_ctx* c = new (std::nothrow) hmpc_ctx();
+  if (!c) return HMPC_ERR_NOMEM;
+  c->variant = variant; c->N = N; c->device = device;
+  c->t = t; c->m = m; c->g = g; c->mu = mu;
+  memcpy(c->Jinv, Jinv, sizeof(c->Jinv));
+  memcpy(c->rh, rh, sizeof(c->rh));
+  c->uref_mode = uref_mode;
+  *out = c;
+  return HMPC_OK;
+}
+
+int hmpc_destroy(hmpc_ctx* c) {
+  if (!c) return HMPC_ERR_ARG;
+  hipSetDevice(c->device);
+  if (c->dbuf) hipFree(c->dbuf);
+  if (c->scratch_i32) hipFree(c->scratch_i32);
+  if (c->own_stream) hipStreamDestroy(c->own_stream);
+  delete c;
+  return HMPC_OK;
+}
+
+const char* hmpc_last_error(hmpc_ctx* c) { return c ? c->err.c_str() : ""; }
+
+int hmpc_solve_batch(hmpc_ctx* c, int64_t B, const double* x_in, const double* x_lin,
+                     const double* x_ref, const double* pf, const double* C, const double* mu,
+                     double* u, double* x, double* obj, int32_t* status, int32_t* iters,
+                     void* stream) {
+  int rc = check_solve_args(c, B, x_in, x_lin, x_ref, pf, C, u, status);
+  if (rc != HMPC_OK || B == 0) return rc;
+  HMPC_HIP(c, hipSetDevice(c->device));
+  hmpc::SolveArgs a = make_args(c, B, x_in, x_lin, x_ref, pf, C, mu, u, x, obj, status, iters, 0);
+  if (!hmpc::launch_solve(c->variant, c->N, a, (hipStream_t)stream)) return HMPC_ERR_UNSUPPORTED;
+  HMPC_HIP(c, hipGetLastError());
+  return HMPC_OK;
+}
+
+int hmpc_time_solve_batch(hmpc_ctx* c, int64_t B, const double* x_in, const double* x_lin,
+                          const double* x_ref, const double* pf, const double* C,
+                          const double* mu, double* u, double* x, double* obj, int32_t* status,
+                          int32_t* iters, int reps, void* stream, double* ms) {
+  int rc = check_solve_args(c, B, x_in, x_lin, x_ref, pf, C, u, status);
+  if (rc != HMPC_OK) return rc;
+  if (reps <= 0 || !ms || B == 0) return HMPC_ERR_ARG;
+  HMPC_HIP(c, hipSetDevice(c->device));
+  hipStream_t s = (hipStream_t)stream;
+  hipEvent_t e0, e1;
+  HMPC_HIP(c, hipEventCreate(&e0));
+  HMPC_HIP(c, hipEventCreate(&e1));
+  hmpc::SolveArgs a = make_args(c, B, x_in, x_lin, x_ref, pf, C, mu, u, x, obj, status, iters, 0);
+  HMPC_HIP(c, hipEventRecord(e0, s));
+  for (int r = 0; r < reps; ++r) hmpc::launch_solve(c->variant, c->N, a, s);
+  HMPC_HIP(c, hipEventRecord(e1, s));
+  HMPC_HIP(c, hipEventSynchronize(e1));
+  float t = 0.f;
+  HMPC_HIP(c, hipEventElapsedTime(&t, e0, e1));
+  hipEventDestroy(e0);
+  hipEventDestroy(e1);
+  *ms = (double)t / reps;
+  HMPC_HIP(c, hipGetLastError());
+  return HMPC_OK;
+}
+
+int hmpc_solve_batch_host(hmpc_ctx* c, int64_t B, const double* x_in, const double* x_lin,
+                          const double* x_ref, const double* pf, const double* C,
+                          const double* mu, double* u, double* x, double* obj, int32_t* status,
+                          int32_t* iters) {
+  int rc = check_solve_args(c, B, x_in, x_lin, x_ref, pf, C, u, status);
+  if (rc != HMPC_OK || B == 0) return rc;
+  HMPC_HIP(c, hipSetDevice(c->device));
+  const int N = c->N;
+  const size_t nd_in = 12 + 12 * (N + 1) + 12 * N + 3 * N + N + 1;
+  const size_t nd_out = 6 * N + 12 * (N + 1) + 1;
+  const size_t bytes = (size_t)B * (8 * (nd_in + nd_out) + 8) + 256;
+  if (bytes > c->dbuf_bytes) {
+    if (c->dbuf) hipFree(c->dbuf);
+    c->dbuf = nullptr;
+    c->dbuf_bytes = 0;
+    HMPC_HIP(c, hipMalloc(&c->dbuf, bytes));
+    c->dbuf_bytes = bytes;
+  }
+  if (!c->own_stream) HMPC_HIP(c, hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking));
+  hipStream_t s = c->own_stream;
+  double* p = (double*)c->dbuf;
+  double* d_xin = p; p += B * 12;
+  double* d_xlin = p; p += B * 12 * (N + 1);
+  double* d_xref = p; p += B * 12 * N;
+  double* d_pf = p; p += B * 3 * N;
+  double* d_C = p; p += B * N;
+  double* d_mu = p; p += B;
+  double* d_u = p; p += B * 6 * N;
+  double* d_x = p; p += B * 12 * (N + 1);
+  double* d_obj = p; p += B;
+  int32_t* d_st = (int32_t*)p;
+  int32_t* d_it = d_st + B;
+  HMPC_HIP(c, hipMemcpyAsync(d_xin, x_in, 8 * B * 12, hipMemcpyHostToDevice, s));
+  HMPC_HIP(c, hipMemcpyAsync(d_xlin, x_lin, 8 * B * 12 * (N + 1), hipMemcpyHostToDevice, s));
+  HMPC_HIP(c, hipMemcpyAsync(d_xref, x_ref, 8 * B * 12 * N, hipMemcpyHostToDevice, s));
+  HMPC_HIP(c, hipMemcpyAsync(d_pf, pf, 8 * B * 3 * N, hipMemcpyHostToDevice, s));
+  HMPC_HIP(c, hipMemcpyAsync(d_C, C, 8 * B * N, hipMemcpyHostToDevice, s));
+  if (mu) HMPC_HIP(c, hipMemcpyAsync(d_mu, mu, 8 * B, hipMemcpyHostToDevice, s));
+  hmpc::SolveArgs a = make_args(c, B, d_xin, d_xlin, d_xref, d_pf, d_C, mu ? d_mu : nullptr,
+                                d_u, d_x, d_obj, d_st, d_it, 0);
+  if (!hmpc::launch_solve(c->variant, c->N, a, s)) return HMPC_ERR_UNSUPPORTED;
+  HMPC_HIP(c, hipGetLastError());
+  HMPC_HIP(c, hipMemcpyAsync(u, d_u, 8 * B * 6 * N, hipMemcpyDeviceToHost, s));
+  if (x) HMPC_HIP(c, hipMemcpyAsync(x, d_x, 8 * B * 12 * (N + 1), hipMemcpyDeviceToHost, s));
+  if (obj) HMPC_HIP(c, hipMemcpyAsync(obj, d_obj, 8 * B, hipMemcpyDeviceToHost, s));
+  HMPC_HIP(c, hipMemcpyAsync(status, d_st, 4 * B, hipMemcpyDeviceToHost, s));
+  if (iters) HMPC_HIP(c, hipMemcpyAsync(iters, d_it, 4 * B, hipMemcpyDeviceToHost, s));
+  HMPC_HIP(c, hipStreamSynchronize(s));
+  return HMPC_OK;
+}
+
+int hmpc_mpcontrol_batch(hmpc_ctx* c, int64_t B, int init, const double* x_in,
+                         const double* x_ref, const double* pf, const double* C,
+                         const double* mu, double* x_prev, double* u, double* obj,
+                         int32_t* status, int32_t* iters, void* stream) {
+  int rc = check_solve_args(c, B, x_in, x_prev, x_ref, pf, C, u, status);
+  if (rc != HMPC_OK || B == 0) return rc;
+  HMPC_HIP(c, hipSetDevice(c->device));
+  hipStream_t s = (hipStream_t)stream;
+  if (init) {
+    if (B > c->scratch_n) {
+      if (c->scratch_i32) hipFree(c->scratch_i32);
+      c->scratch_i32 = nullptr;
+      c->scratch_n = 0;
+      HMPC_HIP(c, hipMalloc(&c->scratch_i32, 8 * B));
+      c->scratch_n = B;
+    }
+    int32_t* s1 = c->scratch_i32;
+    int32_t* i1 = c->scratch_i32 + B;
+    // pass 1: linearise about [x_in; x_ref]  (src/mpc_cvx_euler_3f.py:50-58)
+    hmpc::SolveArgs a1 = make_args(c, B, x_in, x_prev, x_ref, pf, C, mu, u, x_prev, nullptr, s1,
+                                   i1, 1);
+    if (!hmpc::launch_solve(c->variant, c->N, a1, s)) return HMPC_ERR_UNSUPPORTED;
+    // pass 2: linearise about x* of pass 1 (in place: each workgroup stages
+    // its x_lin in LDS before writing x*)
+    hmpc::SolveArgs a2 = make_args(c, B, x_in, x_prev, x_ref, pf, C, mu, u, x_prev, obj, status,
+                                   iters, 0);
+    hmpc::launch_solve(c->variant, c->N, a2, s);
+    const int tpb = 256;
+    hipLaunchKernelGGL(combine_status, dim3((unsigned)((B + tpb - 1) / tpb)), dim3(tpb), 0, s, B,
+                       s1, i1, status, iters);
+  } else {
+    // time shift of the previous x*  (src/mpc_cvx_euler_3f.py:59-62)
+    hmpc::SolveArgs a = make_args(c, B, x_in, x_prev, x_ref, pf, C, mu, u, x_prev, obj, status,
+                                  iters, 2);
+    if (!hmpc::launch_solve(c->variant, c->N, a, s)) return HMPC_ERR_UNSUPPORTED;
+  }
+  HMPC_HIP(c, hipGetLastError());
+  return HMPC_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,201 @@
+"""ctypes binding of libhmpc.so -- the C ABI in include/hmpc.h.
+
+This is the host side of the drop-in boundary: plain pointers and sizes go
+through the C ABI, PyTorch is used only as a device-memory/stream provider
+(``torch.Tensor.data_ptr()``) when the caller keeps its batch on the GPU.
+There is no CPU fallback anywhere in this module: if the shared library or a
+GPU is missing, every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get('HMPC_LIB', os.path.join(HERE, 'libhmpc.so'))
+
+HMPC_OK = 0
+ERRORS = {-1: 'HMPC_ERR_ARG', -2: 'HMPC_ERR_UNSUPPORTED', -3: 'HMPC_ERR_HIP', -4: 'HMPC_ERR_NOMEM'}
+STATUS = {0: 'solved', 1: 'max_iter', 2: 'primal_infeasible', 3: 'numerical'}
+VARIANTS = {'3f': 3, '2f': 2, 3: 3, 2: 2}
+UREF = {'aliased': 0, 'per_stage': 1}
+
+# symbol -> (restype, argtypes); every symbol declared in include/hmpc.h
+_D = ctypes.POINTER(ctypes.c_double)
+_I32 = ctypes.POINTER(ctypes.c_int32)
+_VP = ctypes.c_void_p
+SIGNATURES = {
+    'hmpc_version': (ctypes.c_int, []),
+    'hmpc_supported_horizons': (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.c_int]),
+    'hmpc_create': (ctypes.c_int, [ctypes.POINTER(_VP), ctypes.c_int, ctypes.c_int, ctypes.c_double,
+                                   ctypes.c_double, ctypes.c_double, ctypes.c_double, _D, _D,
+                                   ctypes.c_int, ctypes.c_int]),
+    'hmpc_destroy': (ctypes.c_int, [_VP]),
+    'hmpc_solve_batch': (ctypes.c_int, [_VP, ctypes.c_int64] + [_VP] * 11 + [_VP]),
+    'hmpc_solve_batch_host': (ctypes.c_int, [_VP, ctypes.c_int64] + [_VP] * 11),
+    'hmpc_mpcontrol_batch': (ctypes.c_int, [_VP, ctypes.c_int64, ctypes.c_int] + [_VP] * 10 + [_VP]),
+    'hmpc_last_error': (ctypes.c_char_p, [_VP]),
+    'hmpc_time_solve_batch': (ctypes.c_int, [_VP, ctypes.c_int64] + [_VP] * 11
+                              + [ctypes.c_int, _VP, ctypes.POINTER(ctypes.c_double)]),
+}
+
+_lib = None
+
+
+def load(path: str | None = None):
+    """Load libhmpc.so (built in-tree by build.sh); raises if absent."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise RuntimeError(f'libhmpc.so not found at {p}: run hopper-mpc-inertial_amd/build.sh '
+                           '(there is no CPU fallback)')
+    lib = ctypes.CDLL(p)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def supported_horizons(variant='3f'):
+    lib = load()
+    buf = (ctypes.c_int * 16)()
+    n = lib.hmpc_supported_horizons(VARIANTS[variant], buf, 16)
+    return [buf[i] for i in range(min(n, 16))]
+
+
+def _ptr(a):
+    if a is None:
+        return None
+    if hasattr(a, 'data_ptr'):
+        return ctypes.c_void_p(a.data_ptr())
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+class HmpcError(RuntimeError):
+    pass
+
+
+class Context:
+    """One device-side ``Mpc`` (src/mpc_cvx_euler_3f.py:12-39) for a fixed
+    (variant, N) and the Runner's physical constants."""
+
+    def __init__(self, variant='3f', N=10, t=0.02, m=7.5, g=9.807, mu=1.0, Jinv=None, rh=None,
+                 uref_mode='aliased', device=0):
+        lib = load()
+        if Jinv is None or rh is None:
+            raise ValueError('Jinv and rh are required')
+        self.variant = VARIANTS[variant]
+        self.N = int(N)
+        self.device = int(device)
+        J = np.ascontiguousarray(np.asarray(Jinv, dtype=np.float64).reshape(9))
+        r = np.ascontiguousarray(np.asarray(rh, dtype=np.float64).reshape(3))
+        h = ctypes.c_void_p()
+        rc = lib.hmpc_create(ctypes.byref(h), self.variant, self.N, float(t), float(m), float(g),
+                             float(mu), J.ctypes.data_as(_D), r.ctypes.data_as(_D),
+                             UREF[uref_mode], self.device)
+        if rc != HMPC_OK:
+            raise HmpcError(f'hmpc_create({variant}, N={N}) failed: {ERRORS.get(rc, rc)}')
+        self._h = h
+        self._lib = lib
+
+    def close(self):
+        if getattr(self, '_h', None):
+            self._lib.hmpc_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc, what):
+        if rc != HMPC_OK:
+            msg = self._lib.hmpc_last_error(self._h).decode()
+            raise HmpcError(f'{what} failed: {ERRORS.get(rc, rc)} {msg}')
+
+    # -- host arrays (numpy): synchronous ------------------------------------
+    def solve_host(self, x_in, x_lin, x_ref, pf, C, mu=None):
+        N = self.N
+        c = lambda a: np.ascontiguousarray(np.asarray(a, dtype=np.float64))  # noqa: E731
+        x_in, x_lin, x_ref, pf, C = c(x_in), c(x_lin), c(x_ref), c(pf), c(C)
+        B = x_in.shape[0]
+        assert x_in.shape == (B, 12) and x_lin.shape == (B, N + 1, 12)
+        assert x_ref.shape == (B, N, 12) and pf.shape == (B, N, 3) and C.shape == (B, N)
+        mu_a = None if mu is None else c(np.broadcast_to(np.asarray(mu, dtype=np.float64), (B,)))
+        u = np.empty((B, N, 6))
+        x = np.empty((B, N + 1, 12))
+        obj = np.empty(B)
+        st = np.empty(B, dtype=np.int32)
+        it = np.empty(B, dtype=np.int32)
+        rc = self._lib.hmpc_solve_batch_host(self._h, B, _ptr(x_in), _ptr(x_lin), _ptr(x_ref),
+                                             _ptr(pf), _ptr(C), _ptr(mu_a), _ptr(u), _ptr(x),
+                                             _ptr(obj), _ptr(st), _ptr(it))
+        self._check(rc, 'hmpc_solve_batch_host')
+        return dict(u=u, x=x, obj=obj, status=st, iters=it)
+
+    # -- device tensors (torch, already on this context's GPU): async --------
+    def solve_device(self, x_in, x_lin, x_ref, pf, C, mu=None, out=None, stream=None):
+        import torch
+        N = self.N
+        B = x_in.shape[0]
+        for t_, shp in ((x_in, (B, 12)), (x_lin, (B, N + 1, 12)), (x_ref, (B, N, 12)),
+                        (pf, (B, N, 3)), (C, (B, N))):
+            if tuple(t_.shape) != shp or t_.dtype != torch.float64 or not t_.is_cuda \
+                    or not t_.is_contiguous():
+                raise ValueError(f'expected contiguous float64 cuda tensor of shape {shp}')
+        if out is None:
+            dev = x_in.device
+            out = dict(u=torch.empty((B, N, 6), dtype=torch.float64, device=dev),
+                       x=torch.empty((B, N + 1, 12), dtype=torch.float64, device=dev),
+                       obj=torch.empty(B, dtype=torch.float64, device=dev),
+                       status=torch.empty(B, dtype=torch.int32, device=dev),
+                       iters=torch.empty(B, dtype=torch.int32, device=dev))
+        s = stream if stream is not None else torch.cuda.current_stream(x_in.device).cuda_stream
+        rc = self._lib.hmpc_solve_batch(self._h, B, _ptr(x_in), _ptr(x_lin), _ptr(x_ref), _ptr(pf),
+                                        _ptr(C), _ptr(mu), _ptr(out['u']), _ptr(out.get('x')),
+                                        _ptr(out.get('obj')), _ptr(out['status']),
+                                        _ptr(out.get('iters')), ctypes.c_void_p(s))
+        self._check(rc, 'hmpc_solve_batch')
+        return out
+
+    def mpcontrol_device(self, init, x_in, x_ref, pf, C, x_prev, mu=None, out=None, stream=None):
+        """Batched ``Mpc.mpcontrol`` on device tensors; x_prev (B,N+1,12) is
+        read (init=False) and overwritten with the new x*."""
+        import torch
+        N = self.N
+        B = x_in.shape[0]
+        if out is None:
+            dev = x_in.device
+            out = dict(u=torch.empty((B, N, 6), dtype=torch.float64, device=dev),
+                       obj=torch.empty(B, dtype=torch.float64, device=dev),
+                       status=torch.empty(B, dtype=torch.int32, device=dev),
+                       iters=torch.empty(B, dtype=torch.int32, device=dev))
+        s = stream if stream is not None else torch.cuda.current_stream(x_in.device).cuda_stream
+        rc = self._lib.hmpc_mpcontrol_batch(self._h, B, 1 if init else 0, _ptr(x_in), _ptr(x_ref),
+                                            _ptr(pf), _ptr(C), _ptr(mu), _ptr(x_prev),
+                                            _ptr(out['u']), _ptr(out.get('obj')),
+                                            _ptr(out['status']), _ptr(out.get('iters')),
+                                            ctypes.c_void_p(s))
+        self._check(rc, 'hmpc_mpcontrol_batch')
+        return out
+
+    def time_solve_device(self, x_in, x_lin, x_ref, pf, C, mu, out, reps, stream):
+        """Mean kernel time (ms) over `reps` back-to-back launches, measured
+        with HIP events on `stream` inside the library."""
+        ms = ctypes.c_double()
+        rc = self._lib.hmpc_time_solve_batch(self._h, x_in.shape[0], _ptr(x_in), _ptr(x_lin),
+                                             _ptr(x_ref), _ptr(pf), _ptr(C), _ptr(mu),
+                                             _ptr(out['u']), _ptr(out.get('x')),
+                                             _ptr(out.get('obj')), _ptr(out['status']),
+                                             _ptr(out.get('iters')), int(reps),
+                                             ctypes.c_void_p(stream), ctypes.byref(ms))
+        self._check(rc, 'hmpc_time_solve_batch')
+        return ms.value

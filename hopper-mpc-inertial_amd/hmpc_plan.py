@@ -1,0 +1,157 @@
+"""Reference/gait generation and the synthetic instance sampler.
+
+Host-side restatement of the Runner's planner, used to
+draw the batched synthetic workload of SURVEY.md 8d:
+
+* ``gait_scheduler`` / ``gait_map``   -- src/robotrunner.py:166-180
+* ``path_plan_init``                  -- src/robotrunner.py:182-226, including
+  the ``--curve`` quirks (x column overwritten by the *y* spline, yaw-rate
+  column differentiating itself)
+* ``path_plan_grab``                  -- src/robotrunner.py:228-230
+
+All of it is plain numpy/scipy: it runs once per benchmark outside the timed
+region, never on the solve path.
+"""
+from __future__ import annotations
+
+import dataclasses
+
+import numpy as np
+from scipy.interpolate import CubicSpline
+from scipy.signal import find_peaks
+
+
+@dataclasses.dataclass
+class RunnerConfig:
+    """Runner constants (src/robotrunner.py:32-79)."""
+    dt: float = 1e-3
+    N_run: int = 2000
+    curve: bool = False
+    t_p: float = 0.8
+    phi_switch: float = 0.5
+    N: int = 60
+    mpc_dt: float = 0.02
+    step_adjustment: int = -115
+
+    @property
+    def mpc_factor(self):
+        return int(self.mpc_dt / self.dt)
+
+    @property
+    def N_k(self):
+        return int(self.N * self.mpc_factor)
+
+    @property
+    def t_start(self):
+        return 0.5 * self.t_p * self.phi_switch
+
+    @property
+    def dist(self):
+        return 0.4 * (self.N_run * self.dt)
+
+
+def gait_scheduler(cfg: RunnerConfig, t, t0):
+    phi = np.mod((t - t0) / cfg.t_p, 1)
+    return 0 if phi > cfg.phi_switch else 1
+
+
+def gait_map(cfg: RunnerConfig, N, dt, ts, t0):
+    C = np.zeros(N)
+    for k in range(0, N):
+        C[k] = gait_scheduler(cfg, ts, t0)
+        ts += dt
+    return C
+
+
+def initial_states(cfg: RunnerConfig):
+    """convert(X_0), convert(X_f) for the identity-orientation start/goal
+    (src/robotrunner.py:58-59,91): Euler angles and rates are all zero."""
+    x0 = np.zeros(12)
+    x0[2] = 0.27
+    xf = np.zeros(12)
+    xf[0] = cfg.dist
+    xf[2] = 0.27
+    return x0, xf
+
+
+def path_plan_init(cfg: RunnerConfig, x_in, xf):
+    N_k = cfg.N_k
+    N_run = cfg.N_run
+    dt = cfg.dt
+    t_sit = 0
+    t_traj = int(N_run - t_sit)
+    t_ref = N_run + N_k
+    x_ref = np.linspace(start=x_in, stop=xf, num=t_traj)
+    if cfg.curve is True:
+        spline_t = np.array([0, t_traj * 0.5, t_traj])
+        spline_y = np.array([x_in[1], xf[1] * 0.9, xf[1]])
+        csy = CubicSpline(spline_t, spline_y)
+        spline_psi = np.array([0, -np.sin(45 * np.pi / 180) * 0.4, -np.sin(45 * np.pi / 180)])
+        cspsi = CubicSpline(spline_t, spline_psi)
+        for k in range(t_traj):
+            x_ref[k, 0] = csy(k)     # sic: the reference writes the y spline into column 0
+            x_ref[k, 5] = cspsi(k)
+        x_ref[:-1, 11] = [(x_ref[i + 1, 11] - x_ref[i, 11]) / dt for i in range(N_run - 1)]
+    x_ref = np.vstack((x_ref, np.tile(xf, (N_k + t_sit, 1))))
+    period = cfg.t_p
+    amp = cfg.t_p / 4
+    phi = np.pi * 3 / 2
+    x_ref[:, 2] = [x_in[2] + amp + amp * np.sin(2 * np.pi / period * (i * dt) + phi) for i in range(t_ref)]
+    x_ref[:-1, 6:9] = [(x_ref[i + 1, 0:3] - x_ref[i, 0:3]) / dt for i in range(t_ref - 1)]
+    C = gait_map(cfg, t_ref, dt, cfg.t_start, 0)
+    idx_pf = find_peaks(-x_ref[:, 2])[0] + cfg.step_adjustment
+    idx_pf = np.hstack((0, idx_pf))
+    idx_pf = np.hstack((idx_pf, t_ref - 1))
+    pf_ref = np.zeros((t_ref, 3))
+    kf = 0
+    n_idx = np.shape(idx_pf)[0]
+    for k in range(1, t_ref):
+        if C[k - 1] == 1 and C[k] == 0 and kf < n_idx:
+            kf += 1
+        pf_ref[k, 0:2] = x_ref[idx_pf[kf], 0:2]
+    return x_ref, pf_ref
+
+
+def path_plan_grab(cfg: RunnerConfig, x_ref, k):
+    return x_ref[k:(k + cfg.N_k):cfg.mpc_factor, :]
+
+
+def runner_plan(curve=False, N_run=2000):
+    """The Runner's full plan (N=60 horizon padding) -- the source of every
+    synthetic instance."""
+    cfg = RunnerConfig(N_run=N_run, curve=curve)
+    x0, xf = initial_states(cfg)
+    x_ref, pf_ref = path_plan_init(cfg, x0, xf)
+    return cfg, x_ref, pf_ref
+
+
+def sample_instances(B, N, curve=False, seed=0, mu_sweep=None, N_run=2000):
+    """Draw B synthetic QP instances exactly as SURVEY.md 8d specifies.
+
+    Returns a dict of contiguous float64 arrays:
+      x_in (B,12), x_lin (B,N+1,12) = [x_in; x_ref], x_ref (B,N,12),
+      pf (B,N,3), C (B,N), mu (B,), k0 (B,) int
+    ``mu_sweep=(lo, hi)`` draws mu ~ U(lo, hi), else mu = 1.
+    """
+    cfg, plan, pf_plan = runner_plan(curve=curve, N_run=N_run)
+    rng = np.random.default_rng(seed)
+    f = cfg.mpc_factor
+    k0 = f * rng.integers(0, N_run // f, size=B)
+    noise = np.concatenate([rng.uniform(-0.02, 0.02, (B, 3)),
+                            rng.uniform(-0.05, 0.05, (B, 3)),
+                            rng.uniform(-0.2, 0.2, (B, 6))], axis=1)
+    if mu_sweep is not None:
+        mu = rng.uniform(mu_sweep[0], mu_sweep[1], B)
+    else:
+        mu = np.ones(B)
+    idx = k0[:, None] + f * np.arange(N)[None, :]
+    x_ref = np.ascontiguousarray(plan[idx])
+    pf = np.ascontiguousarray(pf_plan[idx])
+    x_in = plan[k0] + noise
+    # C is a function of k0 only: tabulate per distinct k0
+    C = np.zeros((B, N))
+    for kk in np.unique(k0):
+        C[k0 == kk] = gait_map(cfg, N, cfg.mpc_dt, cfg.t_start + (kk + 1) * cfg.dt, 0)
+    x_lin = np.concatenate([x_in[:, None, :], x_ref], axis=1)
+    return dict(x_in=np.ascontiguousarray(x_in), x_lin=np.ascontiguousarray(x_lin),
+                x_ref=x_ref, pf=pf, C=C, mu=mu, k0=k0)
