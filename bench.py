@@ -1,0 +1,219 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X batched MPC/QP solve path (BASELINE.json metric).
+
+One *step* = one pass of the hot path over one batch: every instance's
+``Mpc.gen_dt_dynamics`` + ``Mpc.build_qp`` + ``Mpc.solve_qp``
+(src/mpc_cvx_euler_3f.py:71-160) on the GPU through the C ABI
+(``hmpc_solve_batch``), then -- for N > 1 ranks -- the RCCL all-gather of the
+per-instance objective and status.  Inputs are resident in HBM
+before the timed region starts.
+
+Default workload = BASELINE.json configs[2]: 65536 randomised instances per
+GPU, 3f, horizon N = 10, --curve reference plan, fp64 (weak scaling: every
+rank solves its own 65536-instance shard of the global batch).
+
+Launch:  python bench.py [--gpus 1] [--steps K] [--warmup W]
+         python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, 'hopper-mpc-inertial_amd')
+sys.path.insert(0, PKG)
+sys.path.insert(0, ROOT)
+
+METRIC = 'QP solves/sec (N=10, 3f) at batch=65k, 1→8 MI355X; max |u*−u*_cvxpy|'
+HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level table)
+
+
+def algorithmic_bytes(N, with_mu=True):
+    """HBM bytes one solve must move: inputs x_in, x_lin,
+    x_ref, pf, C (+ mu), outputs u, x, obj (fp64) and status (int32)."""
+    nin = 12 + 12 * (N + 1) + 12 * N + 3 * N + N + (1 if with_mu else 0)
+    nout = 6 * N + 12 * (N + 1) + 1
+    return 8 * (nin + nout) + 4
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=20)
+    ap.add_argument('--warmup', type=int, default=3)
+    ap.add_argument('--batch', type=int, default=65536, help='instances per GPU')
+    ap.add_argument('--variant', default='3f', choices=['3f', '2f'])
+    ap.add_argument('--N', type=int, default=10)
+    ap.add_argument('--straight', action='store_true', help='straight plan (default: --curve)')
+    ap.add_argument('--mu-sweep', action='store_true', help='mu ~ U(0.3, 1.2)')
+    ap.add_argument('--seed', type=int, default=2024)
+    ap.add_argument('--cpu-seconds', type=float, default=10.0,
+                    help='budget of the bounded CPU-baseline sample (0 disables)')
+    return ap.parse_args()
+
+
+def cpu_baseline(args, inst, gpu_u, gpu_status, budget_s):
+    """Reported baseline, not the target: the CPU oracle (oracle/, a port of
+    the reference's problem construction + an exact fp64 QP solve) timed on
+    a bounded prefix of the same workload on this host, 1 core.  Also
+    returns the parity of those instances against the GPU results."""
+    from oracle import hmpc_oracle as ho
+    if budget_s <= 0:
+        return None, None
+    n = 0
+    du = 0.0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < budget_s and n < len(inst['x_in']):
+        p = ho.MpcParams.runner(args.variant, args.N, mu=float(inst['mu'][n]))
+        s = ho.solve_instance(p, inst['x_in'][n], inst['x_lin'][n], inst['x_ref'][n],
+                              inst['pf'][n], inst['C'][n])
+        if s['status'] == 'solved' and gpu_status[n] == 0:
+            du = max(du, float(np.abs(s['u'] - gpu_u[n]).max()))
+        n += 1
+    el = time.perf_counter() - t0
+    base = {'value': n / el, 'unit': 'QP solves/s', 'cores': 1, 'kind': 'port',
+            'sample': f'first {n} instances of the rank-0 shard, numpy restatement of '
+                      f'gen_dt_dynamics/build_qp + exact fp64 QP solve (oracle/), {el:.1f} s'}
+    parity = {'instances': n, 'max_abs_du': du}
+    return base, parity
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world != args.gpus:
+        raise SystemExit(f'--gpus {args.gpus} but WORLD_SIZE={world}')
+    if not torch.cuda.is_available():
+        raise SystemExit('bench.py needs an MI355X (torch.cuda.is_available() is False)')
+    torch.cuda.set_device(local)
+    dev = torch.device('cuda', local)
+    if world > 1:
+        dist.init_process_group('nccl', device_id=dev)
+
+    import hmpc
+    import hmpc_plan
+    from oracle import hmpc_oracle as ho   # constants only (Runner values)
+
+    N, B = args.N, args.batch
+    inst = hmpc_plan.sample_instances(B, N, curve=not args.straight, seed=args.seed,
+                                      mu_sweep=(0.3, 1.2) if args.mu_sweep else None,
+                                      start=rank * B)
+    d = {k: torch.from_numpy(np.ascontiguousarray(inst[k])).to(dev)
+         for k in ('x_in', 'x_lin', 'x_ref', 'pf', 'C', 'mu')}
+    c = ho.runner_constants()
+    ctx = hmpc.Context(args.variant, N, t=c['t'], m=c['m'], g=c['g'], mu=1.0, Jinv=c['Jinv'],
+                       rh=c['rh'], device=local)
+    out = dict(u=torch.empty((B, N, 6), dtype=torch.float64, device=dev),
+               x=torch.empty((B, N + 1, 12), dtype=torch.float64, device=dev),
+               obj=torch.empty(B, dtype=torch.float64, device=dev),
+               status=torch.empty(B, dtype=torch.int32, device=dev),
+               iters=torch.empty(B, dtype=torch.int32, device=dev))
+    obj_all = torch.empty(B * world, dtype=torch.float64, device=dev)
+    st_all = torch.empty(B * world, dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    def step(ev=None):
+        if ev is not None:
+            ev[0].record(stream)
+        ctx.solve_device(d['x_in'], d['x_lin'], d['x_ref'], d['pf'], d['C'], mu=d['mu'],
+                         out=out, stream=stream.cuda_stream)
+        if ev is not None:
+            ev[1].record(stream)
+        if world > 1:   # the one exchange step: per-instance cost + status
+            dist.all_gather_into_tensor(obj_all, out['obj'])
+            dist.all_gather_into_tensor(st_all, out['status'])
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(evs[k])
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    tt = torch.tensor([el, kern_ms], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    el, kern_ms_max = float(tt[0]), float(tt[1])
+
+    st = out['status'].cpu().numpy()
+    it = out['iters'].cpu().numpy()
+    solved_local = float((st == 0).mean())
+    sf = torch.tensor([solved_local], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(sf, op=dist.ReduceOp.MIN)
+
+    base = parity = None
+    if rank == 0 and world == 1:
+        base, parity = cpu_baseline(args, inst, out['u'].cpu().numpy(), st, args.cpu_seconds)
+
+    if rank == 0:
+        bpsolve = algorithmic_bytes(N)
+        achieved = bpsolve * B / (kern_ms * 1e-3) / 1e9
+        traffic = None
+        tpath = os.path.join(ROOT, 'profiles', 'traffic.json')
+        wl = f'{args.variant}_N{N}_B{B}_{"straight" if args.straight else "curve"}' \
+             f'{"_musweep" if args.mu_sweep else ""}'
+        if os.path.exists(tpath):
+            tj = json.load(open(tpath))
+            traffic = tj.get(wl, {}).get('bytes_per_launch')
+        total = B * world * args.steps
+        rec = {
+            'metric': METRIC,
+            'value': total / el,
+            'unit': 'QP solves/s',
+            'n_gpus': world,
+            'steps': args.steps,
+            'warmup': args.warmup,
+            'ms_per_step': el / args.steps * 1e3,
+            'higher_is_better': True,
+            'scaling': 'weak',
+            'vs_baseline': None,
+            'dtype': 'f64',
+            'data': 'synthetic: Runner path_plan_init plan (--curve) + randomised x0 '
+                    '(SURVEY.md 8d), generated on host, resident in HBM before timing',
+            'config': {'workload': f'configs[2]: batch={B}/GPU randomised x0 + '
+                                   f'{"straight" if args.straight else "--curve"} ref traj, '
+                                   f'{args.variant}, horizon N={N}, fp64'
+                                   f'{", mu sweep" if args.mu_sweep else ""}',
+                       'global_batch': B * world, 'horizon': N, 'variant': args.variant,
+                       'parallelism': f'shard{world}'},
+            'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS,
+                         'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic,
+                         'kernel': f'hmpc::solve_kernel<{args.variant[0]}, {N}>',
+                         'kernel_ms': kern_ms, 'kernel_ms_max_rank': kern_ms_max,
+                         'algorithmic_bytes_per_solve': bpsolve, 'solves_per_launch': B},
+            'cpu_baseline': base,
+            'solved_frac_min_rank': float(sf[0]),
+            'iters_mean': float(it.mean()), 'iters_max': int(it.max()),
+            'parity_sample': parity,
+        }
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    ctx.close()
+
+
+if __name__ == '__main__':
+    main()

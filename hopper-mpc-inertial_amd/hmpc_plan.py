@@ -125,8 +125,32 @@ def runner_plan(curve=False, N_run=2000):
     return cfg, x_ref, pf_ref
 
 
-def sample_instances(B, N, curve=False, seed=0, mu_sweep=None, N_run=2000):
-    """Draw B synthetic QP instances exactly as SURVEY.md 8d specifies.
+BLOCK = 4096   # instances per independent random stream (sharding granule)
+
+
+def _draw_block(seed, blk, n, N_run, f, mu_sweep):
+    """Random draws of instances [blk*BLOCK, blk*BLOCK + n): a function of
+    (seed, blk) only, so any shard of the global batch reproduces them."""
+    rng = np.random.default_rng([seed, blk])
+    k0 = f * rng.integers(0, N_run // f, size=BLOCK)
+    noise = np.concatenate([rng.uniform(-0.02, 0.02, (BLOCK, 3)),
+                            rng.uniform(-0.05, 0.05, (BLOCK, 3)),
+                            rng.uniform(-0.2, 0.2, (BLOCK, 6))], axis=1)
+    if mu_sweep is not None:
+        mu = rng.uniform(mu_sweep[0], mu_sweep[1], BLOCK)
+    else:
+        mu = np.ones(BLOCK)
+    return k0[:n], noise[:n], mu[:n]
+
+
+def sample_instances(B, N, curve=False, seed=0, mu_sweep=None, N_run=2000, start=0):
+    """Draw instances [start, start + B) of the synthetic workload of
+    SURVEY.md 8d.
+
+    Instance i's random draws depend only on (seed, i): a rank that asks for
+    its shard [start, start + B) gets exactly the rows a single process
+    drawing the whole batch would (``start`` must be a multiple of BLOCK
+    unless B covers from the block start).
 
     Returns a dict of contiguous float64 arrays:
       x_in (B,12), x_lin (B,N+1,12) = [x_in; x_ref], x_ref (B,N,12),
@@ -134,16 +158,21 @@ def sample_instances(B, N, curve=False, seed=0, mu_sweep=None, N_run=2000):
     ``mu_sweep=(lo, hi)`` draws mu ~ U(lo, hi), else mu = 1.
     """
     cfg, plan, pf_plan = runner_plan(curve=curve, N_run=N_run)
-    rng = np.random.default_rng(seed)
     f = cfg.mpc_factor
-    k0 = f * rng.integers(0, N_run // f, size=B)
-    noise = np.concatenate([rng.uniform(-0.02, 0.02, (B, 3)),
-                            rng.uniform(-0.05, 0.05, (B, 3)),
-                            rng.uniform(-0.2, 0.2, (B, 6))], axis=1)
-    if mu_sweep is not None:
-        mu = rng.uniform(mu_sweep[0], mu_sweep[1], B)
+    parts = []
+    i = start
+    while i < start + B:
+        blk, off = divmod(i, BLOCK)
+        n = min(BLOCK - off, start + B - i)
+        k0, noise, mu = _draw_block(seed, blk, off + n, N_run, f, mu_sweep)
+        parts.append((k0[off:], noise[off:], mu[off:]))
+        i += n
+    if parts:
+        k0 = np.concatenate([p[0] for p in parts])
+        noise = np.concatenate([p[1] for p in parts])
+        mu = np.concatenate([p[2] for p in parts])
     else:
-        mu = np.ones(B)
+        k0, noise, mu = np.zeros(0, dtype=np.int64), np.zeros((0, 12)), np.zeros(0)
     idx = k0[:, None] + f * np.arange(N)[None, :]
     x_ref = np.ascontiguousarray(plan[idx])
     pf = np.ascontiguousarray(pf_plan[idx])

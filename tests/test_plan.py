@@ -37,3 +37,17 @@ def test_sampler_is_deterministic_and_shaped():
     assert np.array_equal(a['x_lin'][:, 1:], a['x_ref'])
     m = hmpc_plan.sample_instances(64, 20, mu_sweep=(0.3, 1.2), seed=1)['mu']
     assert m.min() >= 0.3 and m.max() <= 1.2
+
+
+def test_sampler_shards_reproduce_the_global_batch():
+    """Instance i depends only on (seed, i): shards drawn by separate ranks
+    concatenate to the single-process batch."""
+    B = 3 * hmpc_plan.BLOCK + 100
+    full = hmpc_plan.sample_instances(B, 10, curve=True, seed=11, mu_sweep=(0.3, 1.2))
+    cuts = [0, 1000, hmpc_plan.BLOCK, 2 * hmpc_plan.BLOCK + 7, B]
+    for lo, hi in zip(cuts[:-1], cuts[1:]):
+        part = hmpc_plan.sample_instances(hi - lo, 10, curve=True, seed=11, mu_sweep=(0.3, 1.2),
+                                          start=lo)
+        for k in full:
+            assert np.array_equal(part[k], full[k][lo:hi]), (k, lo, hi)
+    assert hmpc_plan.sample_instances(0, 10)['x_in'].shape == (0, 12)
