@@ -8,23 +8,25 @@ cd "$(dirname "$0")"
 HIPCC=${HIPCC:-/opt/rocm/bin/hipcc}
 HORIZONS=${HORIZONS:-"5 10 20"}
 JOBS=${JOBS:-8}
+OUT=${OUT:-libhmpc.so}
+BDIR=${BDIR:-build}
 FLAGS="--offload-arch=gfx950 -O3 -fPIC -std=c++17 -Wno-unused-result"
-mkdir -p build
+mkdir -p $BDIR
 LIST=""
 for n in $HORIZONS; do LIST="$LIST X($n)"; done
 pids=()
 for n in $HORIZONS; do
-  $HIPCC $FLAGS -DHMPC_INST_N=$n -c csrc/hmpc_kernels.hip -o build/hmpc_kernels_n$n.o "$@" &
+  $HIPCC $FLAGS -DHMPC_INST_N=$n -c csrc/hmpc_kernels.hip -o $BDIR/hmpc_kernels_n$n.o "$@" &
   pids+=($!)
   while [ "$(jobs -rp | wc -l)" -ge "$JOBS" ]; do sleep 1; done
 done
-$HIPCC $FLAGS "-DHMPC_HORIZON_LIST(X)=$LIST" -c csrc/hmpc_dispatch.cpp -o build/hmpc_dispatch.o &
+$HIPCC $FLAGS "-DHMPC_HORIZON_LIST(X)=$LIST" -c csrc/hmpc_dispatch.cpp -o $BDIR/hmpc_dispatch.o &
 pids+=($!)
-$HIPCC $FLAGS -c csrc/hmpc_capi.cpp -o build/hmpc_capi.o &
+$HIPCC $FLAGS -c csrc/hmpc_capi.cpp -o $BDIR/hmpc_capi.o &
 pids+=($!)
 for p in "${pids[@]}"; do wait "$p"; done
 objs=""
-for n in $HORIZONS; do objs="$objs build/hmpc_kernels_n$n.o"; done
-$HIPCC --offload-arch=gfx950 -shared -fPIC $objs build/hmpc_dispatch.o build/hmpc_capi.o -o libhmpc.so.tmp
-mv libhmpc.so.tmp libhmpc.so
-echo "built $(pwd)/libhmpc.so (horizons: $HORIZONS)"
+for n in $HORIZONS; do objs="$objs $BDIR/hmpc_kernels_n$n.o"; done
+$HIPCC --offload-arch=gfx950 -shared -fPIC $objs $BDIR/hmpc_dispatch.o $BDIR/hmpc_capi.o -o $OUT.tmp
+mv $OUT.tmp $OUT
+echo "built $(pwd)/$OUT (horizons: $HORIZONS)"

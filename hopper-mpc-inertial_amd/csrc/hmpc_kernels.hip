@@ -2,26 +2,39 @@
 //
 // One workgroup of W = ceil(6N/64) wavefronts solves ONE QP instance of the
 // reference's Mpc.build_qp/solve_qp (src/mpc_cvx_euler_3f.py:96-160; 2f
-// :96-158) to its exact optimum.  Lane v of the workgroup owns decision
-// variable v = 6*k + c of the CONDENSED problem (states eliminated through
-// the dynamics), i.e. row v of every NV x NV matrix lives in lane v's
-// registers.  Phases (see DESIGN.md "Kernel"):
+// :96-158) to its exact optimum, on the CONDENSED problem (states eliminated
+// through the dynamics; NV = 6N input variables).  Lane v owns variable
+// v = 6*i + c (stage i, component c).  Phases (DESIGN.md "Kernel"):
 //
 //   0  coalesced load of the instance's inputs into LDS
 //   1  per-stage linearisation = Mpc.gen_dt_dynamics (3f :71-94, 2f :70-94)
-//   2  free response  xbar_{k+1} = Ad_k xbar_k + Gd
-//   3  backward Riccati-like sweep S_t = W_{t-1} + Ad_t' S_{t+1} Ad_t,
-//      Y_j = S_{j+1} Bd_j
-//   4  condensed Hessian rows H[v,:] and gradient h[v] (adjoint sweep)
-//   5  Cholesky H = L L'   (rows in registers, one LDS column per step)
-//   6  J = L^-T            (row v of J built in lane v)
-//   7  unconstrained optimum v0 = -H^-1 h (two triangular sweeps)
-//   8  Goldfarb-Idnani dual active set: the most violated constraint enters,
-//      Householder update of J on add, Givens on drop.  Constraints: torque
-//      box (:123-128), fz box + friction pyramid (:141-146), z >= 0.1
-//      (:129, dense rows over fz through the dynamics); swing / 2f fy
-//      equalities (:134-136, 2f :129) are eliminated as fixed variables.
-//   9  outputs: u* (coalesced), x* by forward simulation, objective incl.
+//   2  wave-uniform sweeps in registers (every lane computes the same values):
+//      free response xbar, gradient terms d_t = W_{t-1}(xbar_t - r_{t-1}),
+//      and the backward cost-to-go S_t = W_{t-1} + Ad_t' S_{t+1} Ad_t.
+//      S_t is block-structured (Ad never mixes translation and rotation and
+//      Q is diagonal): 3 x (p_a, v_a) 2x2 + (yaw, w_z) 2x2 + (roll, pitch,
+//      w_x, w_y) 4x4 = 22 unique entries.
+//   3  lane v builds row v of the condensed Hessian (lower triangle: all the
+//      Cholesky reads) and its gradient entry: the impulse response
+//      e_j = Phi(j+1,i+1) B_i e_c (gradient), the diagonal block from
+//      S_{i+1} B_i e_c, and g_j = Phi(i+1,j+1)' S_{i+1} B_i e_c (j < i).
+//   4  right-looking Cholesky H = L L' with the trailing row in registers.
+//      Every step shifts the row by one register as it updates it, so step k
+//      always reads register 0 and one loop body serves 8 consecutive k (a
+//      runtime loop: the kernel stays small enough for the instruction
+//      cache).  L goes to LDS column-major.
+//   5  unconstrained optimum v0 = -H^-1 h (two triangular sweeps)
+//   6  Goldfarb-Idnani dual active set in range-space form: instead of
+//      J = L^-T Q it keeps an orthonormal basis Qw of L^-1 N_A (lane v holds
+//      row v of Qw in registers) and the triangular R with L^-1 N_A = Qw R
+//      (LDS).  Adding constraint p costs one forward sweep w = L^-1 n_p, a
+//      Gram-Schmidt projection against Qw and one backward sweep
+//      z = L^-T w_perp; dropping one costs Givens rotations on R and Qw.
+//      Constraints: torque box (:123-128), fz box + friction pyramid
+//      (:141-146), z >= 0.1 (:129, dense rows over fz through the dynamics);
+//      swing / 2f fy equalities (:134-136, 2f :129) are eliminated as fixed
+//      variables.
+//   7  outputs: u* (coalesced), x* by forward simulation, objective incl.
 //      its constant term evaluated on (x*, u*), status, iterations.
 //
 // No MFMA: every product is a tiny dense block or a rank-1 update.
@@ -36,8 +49,8 @@
 namespace hmpc {
 
 // compile-time loop: f(std::integral_constant<int, i>) for i in [Begin, End).
-// Every index into a register-resident row (Jr[]) goes through this, so no
-// row ever lands in scratch memory.
+// Every index into a register-resident row goes through this (or the ladders
+// below), so no row ever lands in scratch memory.
 template <int Begin, typename F, int... Is>
 __device__ __forceinline__ void sfor_impl(std::integer_sequence<int, Is...>, F&& f) {
   (f(std::integral_constant<int, Begin + Is>{}), ...);
@@ -46,79 +59,50 @@ template <int Begin, int End, typename F>
 __device__ __forceinline__ void sfor(F&& f) {
   if constexpr (End > Begin) sfor_impl<Begin>(std::make_integer_sequence<int, End - Begin>{}, f);
 }
-// Same, with a scheduling fence every CH iterations: keeps the scheduler from
-// hoisting every LDS load of a long unrolled loop ahead of its FMAs (which
-// would need ~NV extra VGPRs on top of the register-resident row).
-template <int CH, int Begin, int End, typename F>
-__device__ __forceinline__ void sfor_chunked(F&& f) {
-  sfor<Begin, End>([&](auto ic) __attribute__((always_inline)) {
-    constexpr int i = decltype(ic)::value;
-    f(ic);
-    if constexpr (((i - Begin) % CH) == CH - 1) __builtin_amdgcn_sched_barrier(0);
-  });
+// f(l) for l = L, L+1, ... while l < n (n wave-uniform): nested, so the first
+// failing test jumps past every remaining body.
+template <int L, int LMAX, typename F>
+__device__ __forceinline__ void ladder(int n, F&& f) {
+  if constexpr (L < LMAX) {
+    if (L < n) {
+      f(std::integral_constant<int, L>{});
+      ladder<L + 1, LMAX>(n, f);
+    }
+  }
+}
+// f(l) for the single l == n (n wave-uniform).
+template <int L, int LMAX, typename F>
+__device__ __forceinline__ void at_index(int n, F&& f) {
+  if constexpr (L < LMAX) {
+    if (L == n) f(std::integral_constant<int, L>{});
+    else at_index<L + 1, LMAX>(n, f);
+  }
 }
 
 // Empty asm that claims to read and write x: pins the value into a VGPR pair
-// at this point.  Used at step boundaries of the unrolled factorisations so
-// the compiler cannot sink a step's FMAs past the next step's loads (which
-// doubled the live set and spilled the register-resident row to scratch).
+// at this point, so the scheduler cannot sink a step's FMAs past the next
+// step's loads (which would double the live set and spill the row).
 __device__ __forceinline__ void pin(double& x) { asm volatile("" : "+v"(x)); }
-// A wave-uniform 0 the compiler cannot see through.  Added to the LDS
-// address of an iteration's loads, it keeps those loads from being hoisted
-// above the (volatile, hence ordered) point where it is produced -- the
-// scheduler otherwise pulls every iteration's loads of a read-only LDS region
-// to the top of a fully unrolled loop and spills.
+// A wave-uniform 0 the compiler cannot see through.  Added to an LDS address
+// it keeps the loads behind it from being hoisted above this point (the
+// scheduler otherwise pulls every load of a long unrolled loop to the top
+// and spills).
 __device__ __forceinline__ int opaque_zero() {
   int z;
   asm volatile("s_mov_b32 %0, 0" : "=s"(z));
   return z;
 }
-template <int NV>
-__device__ __forceinline__ void pin_row(double (&r)[NV]) {
-  sfor<0, NV>([&](auto jc) __attribute__((always_inline)) { pin(r[decltype(jc)::value]); });
-}
-
-// row[j] += alpha * x[j] for j in [Begin, End), x in LDS.  Loads are issued
-// in chunks of CH behind an opaque zero, and every updated element is pinned,
-// so at most CH loaded values are live beside the row.
-template <int Begin, int End, int CH, int NV>
-__device__ __forceinline__ void row_axpy(double (&row)[NV], double alpha, const double* x) {
-  sfor<Begin, End>([&](auto jc) __attribute__((always_inline)) {
-    constexpr int j = decltype(jc)::value;
-    if constexpr (((j - Begin) % CH) == 0) x += opaque_zero();
-    row[j] = fma(alpha, x[j], row[j]);
-    pin(row[j]);
-  });
-}
-// sum_j row[j] * x[j] for j in [Begin, End), x in LDS, chunked as above.
-template <int Begin, int End, int CH, int NV>
-__device__ __forceinline__ double row_dot(const double (&row)[NV], const double* x) {
-  double s0 = 0.0, s1 = 0.0;
-  sfor<Begin, End>([&](auto jc) __attribute__((always_inline)) {
-    constexpr int j = decltype(jc)::value;
-    if constexpr (((j - Begin) % CH) == 0) {
-      x += opaque_zero();
-      pin(s0);
-      pin(s1);
-    }
-    if constexpr ((j & 1) == 0) s0 = fma(row[j], x[j], s0);
-    else s1 = fma(row[j], x[j], s1);
-  });
-  return s0 + s1;
-}
 
 // ----------------------------------------------------------------------------
 // constants of Mpc.__init__ / build_qp (src/mpc_cvx_euler_3f.py:20,35,37,113-129)
 // ----------------------------------------------------------------------------
-__device__ __forceinline__ double qdiag(int c) {   // Q = diag(50,50,2,1,1,50,1,1,1,10,10,10)
-  return (c == 0 || c == 1 || c == 5) ? 50.0 : (c == 2 ? 2.0 : (c >= 9 ? 10.0 : 1.0));
-}
-constexpr double kRdiag = 0.001;   // R = 0.001 I
-constexpr double kTermQ = 100.0;   // kf at k = N-1
-constexpr double kFzMax = 206.0;   // f_max[2]
-constexpr double kZmin = 0.1;
+constexpr double kQ[12] = {50, 50, 2, 1, 1, 50, 1, 1, 1, 10, 10, 10};   // :35
+constexpr double kRdiag = 0.001;   // R = 0.001 I   (:37)
+constexpr double kTermQ = 100.0;   // kf at k = N-1 (:113)
+constexpr double kFzMax = 206.0;   // f_max[2]      (:20)
+constexpr double kZmin = 0.1;      //               (:129)
 constexpr double kTol = 1e-10;     // scaled primal feasibility tolerance
-__device__ __forceinline__ double tau_lim(int c) { return c == 5 ? 4.0 : 7.78; }
+__device__ __forceinline__ double tau_lim(int c) { return c == 5 ? 4.0 : 7.78; }   // :123-128
 
 constexpr int ST_SOLVED = 0, ST_MAXIT = 1, ST_INFEAS = 2, ST_NUMERICAL = 3;
 
@@ -131,6 +115,7 @@ __device__ __forceinline__ double rdlane(double x, int l) {
   int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
   return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
+__device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
 
 __device__ __forceinline__ double wave_sum(double x) {
 #pragma unroll
@@ -153,8 +138,14 @@ __device__ __forceinline__ void wave_argmin(double& v, int& i) {
 
 template <int W>
 struct Blk {
-  // `red` must hold >= 2*W doubles; every call is bracketed by barriers so
-  // consecutive calls may reuse it.
+  // LDS ordering point.  One wave: LDS instructions of a wave execute in
+  // order, so only the compiler has to be kept from reordering them.
+  __device__ static void sync() {
+    if constexpr (W == 1) __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    else __syncthreads();
+  }
+  // `red` must hold >= 2*W doubles; calls are bracketed by barriers (W > 1)
+  // so consecutive calls may reuse it.
   __device__ static double sum(double x, double* red) {
     x = wave_sum(x);
     if constexpr (W == 1) {
@@ -195,28 +186,20 @@ struct Blk {
       return red[0];
     }
   }
-  // rank of this lane among lanes with flag set, and the total count
-  __device__ static void rank(bool flag, int& r, int& cnt, double* red) {
+  // first lane (over the workgroup) with flag set, or -1
+  __device__ static int first(bool flag, double* red) {
     unsigned long long m = __ballot(flag);
-    int lane = threadIdx.x & 63;
-    r = __popcll(m & ((1ull << lane) - 1ull));
-    cnt = __popcll(m);
+    int f = m ? (int)__builtin_ctzll(m) + (int)(threadIdx.x & ~63u) : 0x7fffffff;
     if constexpr (W > 1) {
       int* ired = reinterpret_cast<int*>(red);
       __syncthreads();
-      if (lane == 0) ired[threadIdx.x >> 6] = cnt;
+      if ((threadIdx.x & 63) == 0) ired[threadIdx.x >> 6] = f;
       __syncthreads();
-      int off = 0, tot = 0;
-      int me = threadIdx.x >> 6;
+      f = ired[0];
 #pragma unroll
-      for (int w = 0; w < W; ++w) {
-        int c = ired[w];
-        if (w < me) off += c;
-        tot += c;
-      }
-      r += off;
-      cnt = tot;
+      for (int w = 1; w < W; ++w) f = ired[w] < f ? ired[w] : f;
     }
+    return f == 0x7fffffff ? -1 : uni(f);
   }
 };
 
@@ -228,47 +211,173 @@ struct Lay {
   static constexpr int NV = 6 * N;
   static constexpr int W = (NV + 63) / 64;
   static constexpr int NT = 64 * W;
-  static constexpr int NSLOT = 4;
+  // active-set capacity (registers for Qw, LDS for R); the largest active set
+  // seen over 65536 random N=10 instances is 12
+  static constexpr int QMAX = NV < 24 ? NV : (N <= 10 ? 24 : 48);
   static constexpr int e2(int n) { return (n + 1) & ~1; }
+  static constexpr int NS = 22;                    // unique entries of S_t
+  static constexpr int LCN = NV * (NV + 1) / 2;    // packed L
   // persistent
-  static constexpr int XIN = 0;
-  static constexpr int CC = XIN + 12;
-  static constexpr int CS = CC + e2(N);
-  static constexpr int BD = CS + 2 * N;           // rows 6..11 of Bd_k: [k][a][col] 6x6
-  static constexpr int XBAR = BD + 36 * N;         // [(N+1)][12]
-  static constexpr int DZ = XBAR + 12 * (N + 1);   // [NT]
-  static constexpr int XS = DZ + NT;               // [NT]
+  static constexpr int XIN = 0;                    // [12]
+  static constexpr int CC = XIN + 12;              // [N] contact schedule
+  static constexpr int CS = CC + e2(N);            // [N][2] cos, sin of yaw
+  static constexpr int BW = CS + 2 * N;            // [N][3][6] rows 9..11 of Bd_k
+  static constexpr int ZB = BW + 18 * N;           // [N+1] free-response heights
+  static constexpr int XS = ZB + e2(N + 1);        // [NT] primal broadcast
   static constexpr int RED = XS + NT;              // [16]
-  static constexpr int UA = RED + 16;              // [NV] multipliers of active constraints
-  static constexpr int RV = UA + NV;               // [NV]
-  static constexpr int ACT = RV + NV;              // [NV] (int storage)
-  static constexpr int SD = ACT + NV;              // [NV] subdiagonal scratch for drops
-  static constexpr int U0 = SD + NV;               // start of the union
-  // union A (phases 0-4)
-  static constexpr int XLIN = U0;                  // [(N+1)][12]
-  static constexpr int XREF = XLIN + 12 * (N + 1); // [N][12]
-  static constexpr int PF = XREF + 12 * N;         // [N][3]
-  static constexpr int SB = PF + e2(3 * N);        // [2][144]
-  static constexpr int YY = SB + 288;              // [N][12][6]
-  static constexpr int ADJ = YY + 72 * N;          // [(N+1)][12]
-  static constexpr int ENDA = ADJ + 12 * (N + 1);
-  // union B (phases 5-9)
-  static constexpr int LP = U0;                    // packed lower L, row r at r(r+1)/2; later R
-  static constexpr int LPS = e2(NV * (NV + 1) / 2 + NT);
-  static constexpr int INVD = LP + LPS;            // [NV]
-  static constexpr int COL = INVD + e2(NV);        // [2][NT]   (also final x* staging)
-  static constexpr int SLOT = COL + 2 * NT;        // [NSLOT][NV]
-  static constexpr int ENDB = SLOT + (NSLOT + 1) * NV;   // + one pad row
-  static constexpr int XOUT = COL;                 // [(N+1)][12] <= 2*NT + NSLOT*NV
+  static constexpr int INVD = RED + 16;            // [NV] 1 / L_kk
+  static constexpr int UA = INVD + e2(NV);         // [QMAX] active multipliers
+  static constexpr int ACT = UA + QMAX;            // [QMAX] active ids (int)
+  static constexpr int CB = ACT + QMAX;            // [QMAX] c = Qw' w
+  static constexpr int GV = CB + QMAX;             // [QMAX][2] Givens of a drop
+  static constexpr int SD = GV + 2 * QMAX;         // [QMAX] subdiagonal scratch
+  static constexpr int RM = SD + QMAX;             // packed upper R, col l at l(l+1)/2
+  static constexpr int COLB = (RM + e2(QMAX * (QMAX + 1) / 2) + 1) & ~1;   // [2][NT+8], 16-B aligned
+  static constexpr int U0 = COLB + 2 * (NT + 8);
+  // union A (phases 0-3)
+  static constexpr int XLIN = U0;                  // [N][12]  rows 0..N-1
+  static constexpr int PF = XLIN + 12 * N;         // [N][3]
+  static constexpr int XREF = PF + e2(3 * N);      // [N][12]
+  static constexpr int SS = XREF + 12 * N;         // [N][22]  S_{t}, t = 1..N
+  static constexpr int DG = SS + NS * N;           // [N][12]  d_t, t = 1..N
+  static constexpr int ENDA = DG + 12 * N;
+  // union B (phases 4-7)
+  static constexpr int LC = U0;                    // L, column-major packed
+  static constexpr int XO = U0;                    // x* staging (after L is dead)
+  static constexpr int ENDB = LC + e2(LCN);
   static constexpr int TOTAL = ENDA > ENDB ? ENDA : ENDB;
-  static_assert(12 * (N + 1) <= 2 * NT + NSLOT * NV, "x* staging does not fit");
+  static_assert(12 * (N + 1) <= LCN, "x* staging does not fit");
+  // start of column k of L (rows k..NV-1)
+  __device__ static int cb(int k) { return k * NV - ((k * (k - 1)) >> 1); }
 };
 
 __device__ __forceinline__ int loff(int r) { return (r * (r + 1)) >> 1; }
 
+// S_t storage order (22 entries):
+//   0..8   per axis a: [pp, pv, vv] at 3a    (p_a = x[a], v_a = x[6+a])
+//   9..11  yaw: [tt, tw, ww]                 (theta_z = x[5], w_z = x[11])
+//   12..21 roll/pitch block y = (x3, x4, x9, x10):
+//          P00 P01 P11 M00 M01 M10 M11 Q00 Q01 Q11  (M_ij = S[x(3+i)][x(9+j)])
+// f = S e for the structured S (full 12 rows)
+__device__ __forceinline__ void s_times(const double* s, const double (&e)[12], double (&f)[12]) {
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    f[a] = s[3 * a] * e[a] + s[3 * a + 1] * e[6 + a];
+    f[6 + a] = s[3 * a + 1] * e[a] + s[3 * a + 2] * e[6 + a];
+  }
+  f[5] = s[9] * e[5] + s[10] * e[11];
+  f[11] = s[10] * e[5] + s[11] * e[11];
+  const double P00 = s[12], P01 = s[13], P11 = s[14], M00 = s[15], M01 = s[16], M10 = s[17],
+               M11 = s[18], Q00 = s[19], Q01 = s[20], Q11 = s[21];
+  f[3] = P00 * e[3] + P01 * e[4] + M00 * e[9] + M01 * e[10];
+  f[4] = P01 * e[3] + P11 * e[4] + M10 * e[9] + M11 * e[10];
+  f[9] = M00 * e[3] + M10 * e[4] + Q00 * e[9] + Q01 * e[10];
+  f[10] = M01 * e[3] + M11 * e[4] + Q01 * e[9] + Q11 * e[10];
+}
+
+// x <- Ad x with Ad = I + dt A(psi): p += dt v; theta += dt Rz(psi) w
+// (src/mpc_cvx_euler_3f.py:27,87,91; rz of src/utils.py:46-51)
+__device__ __forceinline__ void ad_times(double (&x)[12], double dt, double cp, double sp) {
+#pragma unroll
+  for (int a = 0; a < 3; ++a) x[a] = fma(dt, x[6 + a], x[a]);
+  const double w0 = x[9], w1 = x[10];
+  x[3] = x[3] + ((cp * dt) * w0 + (sp * dt) * w1);
+  x[4] = x[4] + ((-sp * dt) * w0 + (cp * dt) * w1);
+  x[5] = fma(dt, x[11], x[5]);
+}
+// g <- Ad' g
+__device__ __forceinline__ void adt_times(double (&g)[12], double dt, double cp, double sp) {
+#pragma unroll
+  for (int a = 0; a < 3; ++a) g[6 + a] = fma(dt, g[a], g[6 + a]);
+  const double g3 = g[3], g4 = g[4];
+  g[9] = g[9] + ((cp * dt) * g3 + (-sp * dt) * g4);
+  g[10] = g[10] + ((sp * dt) * g3 + (cp * dt) * g4);
+  g[11] = fma(dt, g[5], g[11]);
+}
+
+// rows 6..8 of Bd_k, column c2 (< 3): 3f dt/m I (:28), 2f Rz'(psi) dt/m (2f :87)
+template <int VAR>
+__device__ __forceinline__ double bv(int r, int c2, double dtm, double cp, double sp) {
+  if constexpr (VAR == 3) {
+    return r == c2 ? dtm : 0.0;
+  } else {
+    // Rz' = [[c, -s, 0], [s, c, 0], [0, 0, 1]]
+    if (r == 2 || c2 == 2) return (r == c2) ? dtm : 0.0;
+    if (r == c2) return cp * dtm;
+    return (r == 0) ? -sp * dtm : sp * dtm;
+  }
+}
+
+// 2 Bd_j[:, c2]' y[6..11]  (rows 0..5 of Bd are zero)
+template <int VAR>
+__device__ __forceinline__ double bd_dot(int c2, const double (&y)[12], const double* bw, double dtm,
+                                         double cp, double sp) {
+  double acc = 0.0;
+  if (c2 < 3) {
+#pragma unroll
+    for (int r = 0; r < 3; ++r) acc = fma(bv<VAR>(r, c2, dtm, cp, sp), y[6 + r], acc);
+  }
+#pragma unroll
+  for (int r = 0; r < 3; ++r) acc = fma(bw[6 * r + c2], y[9 + r], acc);
+  return 2.0 * acc;
+}
+
+// ----------------------------------------------------------------------------
+// triangular sweeps with L column-major packed in LDS (lane v = row v)
+// ----------------------------------------------------------------------------
+// y = L^-1 b (lane v holds b_v); rows before s0 are zero
+template <int N>
+__device__ __forceinline__ double tri_fwd(double acc, int s0, const double* Lc,
+                                          const double* invd, double* red) {
+  using L = Lay<N>;
+  constexpr int NV = L::NV;
+  const int tid = threadIdx.x;
+  double y = 0.0;
+#pragma unroll 1
+  for (int s = s0; s < NV; ++s) {
+    const bool below = tid > s && tid < NV;
+    double l = Lc[L::cb(s) + (below ? tid - s : 0)];
+    const double ys = Blk<L::W>::bcast(acc, s, red) * invd[s];
+    if (tid == s) y = ys;
+    if (!below) l = 0.0;
+    acc = fma(-l, ys, acc);
+  }
+  return y;
+}
+// z = L^-T b (lane v holds b_v)
+template <int N>
+__device__ __forceinline__ double tri_bwd(double acc, const double* Lc, const double* invd,
+                                          double* red) {
+  using L = Lay<N>;
+  constexpr int NV = L::NV;
+  const int tid = threadIdx.x;
+  double z = 0.0;
+#pragma unroll 1
+  for (int s = NV - 1; s >= 0; --s) {
+    const int vv = tid < s ? tid : 0;
+    double l = Lc[L::cb(vv) + s - vv];
+    const double zs = Blk<L::W>::bcast(acc, s, red) * invd[s];
+    if (tid == s) z = zs;
+    if (!(tid < s)) l = 0.0;
+    acc = fma(-l, zs, acc);
+  }
+  return z;
+}
+
 // ----------------------------------------------------------------------------
 // the kernel
 // ----------------------------------------------------------------------------
+// Diagnostic build only (-DHMPC_STAMPS, tools/phase_stamps.py): s_memtime at
+// every phase boundary, written over the instance's x* row at the end.  The
+// product build compiles these to nothing.
+#ifdef HMPC_STAMPS
+#define HMPC_STAMP(i) (stamp_[i] = __builtin_amdgcn_s_memtime())
+#elif defined(HMPC_MARKS)   // phase markers in the .s (register-pressure work)
+#define HMPC_STAMP(i) asm volatile(";@@PHASE " #i)
+#else
+#define HMPC_STAMP(i) ((void)0)
+#endif
+
 #ifndef HMPC_WAVES_PER_EU
 #define HMPC_WAVES_PER_EU(W) ((W) == 1 ? 2 : 1)
 #endif
@@ -279,14 +388,20 @@ solve_kernel(SolveArgs a) {
   constexpr int NV = L::NV;
   constexpr int W = L::W;
   constexpr int NT = L::NT;
+  constexpr int QMAX = L::QMAX;
   using B = Blk<W>;
-  __shared__ double sm[L::TOTAL];
+  __shared__ __attribute__((aligned(16))) double sm[L::TOTAL];
   double* red = sm + L::RED;
+#ifdef HMPC_STAMPS
+  long long stamp_[16] = {0};
+#endif
+  HMPC_STAMP(0);
 
   const int tid = threadIdx.x;
   const int64_t b = blockIdx.x;
   const double dt = a.dt;
   const double mu = a.mu ? a.mu[b] : a.mu_default;
+  const double dtm = dt / a.m;
 
   // ---------------- phase 0: coalesced loads --------------------------------
   for (int i = tid; i < 12; i += NT) sm[L::XIN + i] = a.x_in[b * 12 + i];
@@ -294,22 +409,19 @@ solve_kernel(SolveArgs a) {
   for (int i = tid; i < 3 * N; i += NT) sm[L::PF + i] = a.pf[b * 3 * N + i];
   for (int i = tid; i < N; i += NT) sm[L::CC + i] = a.C[b * N + i];
   if (a.shift_mode == 0) {
-    for (int i = tid; i < 12 * (N + 1); i += NT) sm[L::XLIN + i] = a.x_lin[b * 12 * (N + 1) + i];
+    for (int i = tid; i < 12 * N; i += NT) sm[L::XLIN + i] = a.x_lin[b * 12 * (N + 1) + i];
   } else if (a.shift_mode == 1) {   // [x_in; x_ref]          (3f :52-53)
-    for (int i = tid; i < 12 * (N + 1); i += NT)
+    for (int i = tid; i < 12 * N; i += NT)
       sm[L::XLIN + i] = i < 12 ? a.x_in[b * 12 + i] : a.x_ref[b * 12 * N + i - 12];
   } else {                          // [x_in; x_prev[2:]; x_prev[N]]  (3f :59-62)
     const double* xp = a.x_lin + b * 12 * (N + 1);
-    for (int i = tid; i < 12 * (N + 1); i += NT) {
-      int r = i / 12, c = i - 12 * r;
-      double v;
-      if (r == 0) v = a.x_in[b * 12 + c];
-      else if (r < N) v = xp[(r + 1) * 12 + c];
-      else v = xp[N * 12 + c];
-      sm[L::XLIN + i] = v;
+    for (int i = tid; i < 12 * N; i += NT) {
+      const int r = i / 12, c = i - 12 * r;
+      sm[L::XLIN + i] = (r == 0) ? a.x_in[b * 12 + c] : xp[(r + 1) * 12 + c];   // r+1 <= N
     }
   }
   __syncthreads();
+  HMPC_STAMP(1);
 
   // ---------------- phase 1: gen_dt_dynamics (lane k < N) -------------------
   if (tid < N) {
@@ -322,6 +434,7 @@ solve_kernel(SolveArgs a) {
     double d[3], rf[3];
 #pragma unroll
     for (int i = 0; i < 3; ++i) d[i] = sm[L::PF + 3 * k + i] - sm[L::XLIN + 12 * k + i];
+    // rf = rh + Rz (pf - p)   (:84)
 #pragma unroll
     for (int i = 0; i < 3; ++i) rf[i] = a.rh[i] + (Rz[i][0] * d[0] + Rz[i][1] * d[1] + Rz[i][2] * d[2]);
     double T[3][3], Jw[3][3], RzT[3][3];
@@ -329,6 +442,7 @@ solve_kernel(SolveArgs a) {
     for (int i = 0; i < 3; ++i)
 #pragma unroll
       for (int j = 0; j < 3; ++j) RzT[i][j] = Rz[j][i];
+    // J_w_inv = Rz Jinv Rz'   (:86)
 #pragma unroll
     for (int i = 0; i < 3; ++i)
 #pragma unroll
@@ -338,19 +452,21 @@ solve_kernel(SolveArgs a) {
     for (int i = 0; i < 3; ++i)
 #pragma unroll
       for (int j = 0; j < 3; ++j) Jw[i][j] = T[i][0] * RzT[0][j] + T[i][1] * RzT[1][j] + T[i][2] * RzT[2][j];
-    double Bwt[3][3], Bwf[3][3], Bvf[3][3];
+    double Bwt[3][3], Bwf[3][3];
+    // B[9:12, 3:6] = J_w_inv Rz'   (:89)
 #pragma unroll
     for (int i = 0; i < 3; ++i)
 #pragma unroll
       for (int j = 0; j < 3; ++j) Bwt[i][j] = Jw[i][0] * RzT[0][j] + Jw[i][1] * RzT[1][j] + Jw[i][2] * RzT[2][j];
     double w[3];
-    if constexpr (VAR == 3) {   // rhat = hat(Rz' rf); B[9:12,0:3] = Jw rhat; B[6:9,0:3] = I/m
+    if constexpr (VAR == 3) {   // rhat = hat(Rz' rf); B[9:12,0:3] = Jw rhat   (:85,88)
 #pragma unroll
       for (int i = 0; i < 3; ++i) w[i] = RzT[i][0] * rf[0] + RzT[i][1] * rf[1] + RzT[i][2] * rf[2];
-    } else {                    // rhat = hat(rf); B[9:12,0:3] = (Jw Rz') rhat; B[6:9,0:3] = Rz'/m
+    } else {                    // rhat = hat(rf); B[9:12,0:3] = (Jw Rz') rhat   (2f :84,88)
 #pragma unroll
       for (int i = 0; i < 3; ++i) w[i] = rf[i];
     }
+    // hat (src/utils.py:21-25)
     const double hw[3][3] = {{0.0, -w[2], w[1]}, {w[2], 0.0, -w[0]}, {-w[1], w[0], 0.0}};
 #pragma unroll
     for (int i = 0; i < 3; ++i)
@@ -361,123 +477,99 @@ solve_kernel(SolveArgs a) {
         else
           Bwf[i][j] = Bwt[i][0] * hw[0][j] + Bwt[i][1] * hw[1][j] + Bwt[i][2] * hw[2][j];
       }
-    const double im = 1.0 / a.m;
-#pragma unroll
-    for (int i = 0; i < 3; ++i)
-#pragma unroll
-      for (int j = 0; j < 3; ++j) Bvf[i][j] = (VAR == 3) ? (i == j ? im : 0.0) : RzT[i][j] / a.m;
-    double* bd = sm + L::BD + 36 * k;
+    double* bw = sm + L::BW + 18 * k;
 #pragma unroll
     for (int i = 0; i < 3; ++i)
 #pragma unroll
       for (int j = 0; j < 3; ++j) {
-        bd[i * 6 + j] = Bvf[i][j] * dt;
-        bd[i * 6 + 3 + j] = 0.0;
-        bd[(3 + i) * 6 + j] = Bwf[i][j] * dt;
-        bd[(3 + i) * 6 + 3 + j] = Bwt[i][j] * dt;
+        bw[i * 6 + j] = Bwf[i][j] * dt;
+        bw[i * 6 + 3 + j] = Bwt[i][j] * dt;
       }
     sm[L::CS + 2 * k] = cp;
     sm[L::CS + 2 * k + 1] = sp;
   }
   __syncthreads();
+  HMPC_STAMP(2);
 
-  // ---------------- phase 2: free response (lanes 0..11 of wave 0) ----------
+  // ---------------- phase 2: wave-uniform sweeps ----------------------------
   {
-    double xv = tid < 12 ? sm[L::XIN + tid] : 0.0;
-    if (tid < 12) sm[L::XBAR + tid] = xv;
+    // free response xbar_{k+1} = Ad_k xbar_k + Gd and gradient terms
+    // d_{k+1} = W_k (xbar_{k+1} - r_k)
+    double xb[12];
+#pragma unroll
+    for (int r = 0; r < 12; ++r) xb[r] = sm[L::XIN + r];
+    if (tid == 0) sm[L::ZB] = xb[2];
+#pragma unroll 1
     for (int k = 0; k < N; ++k) {
       const double cp = sm[L::CS + 2 * k], sp = sm[L::CS + 2 * k + 1];
-      const double vsrc = __shfl(xv, (tid + 6) & 63, 64);
-      const double w0 = __shfl(xv, 9, 64), w1 = __shfl(xv, 10, 64), w2 = __shfl(xv, 11, 64);
-      double nx = xv;
-      if (tid < 3) nx = xv + dt * vsrc;
-      else if (tid == 3) nx = xv + ((cp * dt) * w0 + (sp * dt) * w1);
-      else if (tid == 4) nx = xv + ((-sp * dt) * w0 + (cp * dt) * w1);
-      else if (tid == 5) nx = xv + dt * w2;
-      else if (tid == 8) nx = xv + (-a.g * dt);
-      xv = nx;
-      if (tid < 12) sm[L::XBAR + 12 * (k + 1) + tid] = xv;
-    }
-  }
-  // (XBAR is consumed after the next barrier)
-
-  // ---------------- phase 3: S sweep, Y_j = S_{j+1} Bd_j --------------------
-  {
-    // S_N = W_{N-1} = kTermQ * Q
-    for (int e = tid; e < 144; e += NT) {
-      int r = e / 12, c = e - 12 * r;
-      sm[L::SB + e] = (r == c) ? kTermQ * qdiag(r) : 0.0;
-    }
-    __syncthreads();
-    int cur = 0;
-    for (int t = N; t >= 1; --t) {
-      const double* S = sm + L::SB + 144 * cur;
-      // Y_{t-1} = S_t[:, 6:12] * Bd_{t-1}
-      const double* bd = sm + L::BD + 36 * (t - 1);
-      double* Y = sm + L::YY + 72 * (t - 1);
-      for (int e = tid; e < 72; e += NT) {
-        int r = e / 6, c = e - 6 * r;
-        double acc = 0.0;
+      ad_times(xb, dt, cp, sp);
+      xb[8] += -a.g * dt;
+      const double kf = (k == N - 1) ? kTermQ : 1.0;
+      if (tid == 0) {
+        sm[L::ZB + k + 1] = xb[2];
 #pragma unroll
-        for (int q = 0; q < 6; ++q) acc += S[12 * r + 6 + q] * bd[6 * q + c];
-        Y[e] = acc;
+        for (int r = 0; r < 12; ++r) sm[L::DG + 12 * k + r] = kf * kQ[r] * (xb[r] - sm[L::XREF + 12 * k + r]);
       }
-      if (t > 1) {
-        // S_{t-1} = W_{t-2} + Ad_{t-1}' S_t Ad_{t-1}
-        const int ti = t - 1;
-        const double cp = sm[L::CS + 2 * ti], sp = sm[L::CS + 2 * ti + 1];
-        double* Sn = sm + L::SB + 144 * (cur ^ 1);
-        for (int e = tid; e < 144; e += NT) {
-          int r = e / 12, c = e - 12 * r;
-          // column r of Ad = e_r + dt*A[:,r] has at most 3 nonzeros:
-          // (r, 1), and (ra1, ca1), (ra2, ca2) with a zero coefficient when absent
-          int ra1 = 0, ra2 = 0, rb1 = 0, rb2 = 0;
-          double ca1 = 0.0, ca2 = 0.0, cb1 = 0.0, cb2 = 0.0;
-          if (r >= 6 && r < 9) { ra1 = r - 6; ca1 = dt; }
-          if (r == 9) { ra1 = 3; ca1 = cp * dt; ra2 = 4; ca2 = -sp * dt; }
-          if (r == 10) { ra1 = 3; ca1 = sp * dt; ra2 = 4; ca2 = cp * dt; }
-          if (r == 11) { ra1 = 5; ca1 = dt; }
-          if (c >= 6 && c < 9) { rb1 = c - 6; cb1 = dt; }
-          if (c == 9) { rb1 = 3; cb1 = cp * dt; rb2 = 4; cb2 = -sp * dt; }
-          if (c == 10) { rb1 = 3; cb1 = sp * dt; rb2 = 4; cb2 = cp * dt; }
-          if (c == 11) { rb1 = 5; cb1 = dt; }
-          auto row = [&](int ra) {
-            return S[12 * ra + c] + cb1 * S[12 * ra + rb1] + cb2 * S[12 * ra + rb2];
-          };
-          double acc = row(r) + ca1 * row(ra1) + ca2 * row(ra2);
-          if (r == c) acc += qdiag(r);   // W_{t-2}, kf = 1 for t-2 < N-1
-          Sn[e] = acc;
-        }
-        cur ^= 1;
-      }
-      __syncthreads();
     }
-  }
-
-  // ---------------- phase 4a: adjoint sweep (lanes 0..11) -------------------
-  // a_N = W_{N-1}(xbar_N - r_{N-1}); a_t = W_{t-1}(xbar_t - r_{t-1}) + Ad_t' a_{t+1}
-  {
-    double av = 0.0;
-    if (tid < 12)
-      av = kTermQ * qdiag(tid) * (sm[L::XBAR + 12 * N + tid] - sm[L::XREF + 12 * (N - 1) + tid]);
-    if (tid < 12) sm[L::ADJ + 12 * N + tid] = av;
+    // S_N = W_{N-1} = 100 Q; S_t = Q + Ad_t' S_{t+1} Ad_t, t = N-1 .. 1
+    double s[22];
+#pragma unroll
+    for (int a3 = 0; a3 < 3; ++a3) {
+      s[3 * a3] = kTermQ * kQ[a3];
+      s[3 * a3 + 1] = 0.0;
+      s[3 * a3 + 2] = kTermQ * kQ[6 + a3];
+    }
+    s[9] = kTermQ * kQ[5]; s[10] = 0.0; s[11] = kTermQ * kQ[11];
+    s[12] = kTermQ * kQ[3]; s[13] = 0.0; s[14] = kTermQ * kQ[4];
+    s[15] = s[16] = s[17] = s[18] = 0.0;
+    s[19] = kTermQ * kQ[9]; s[20] = 0.0; s[21] = kTermQ * kQ[10];
+    if (tid == 0)
+#pragma unroll
+      for (int e = 0; e < 22; ++e) sm[L::SS + 22 * (N - 1) + e] = s[e];
+#pragma unroll 1
     for (int t = N - 1; t >= 1; --t) {
       const double cp = sm[L::CS + 2 * t], sp = sm[L::CS + 2 * t + 1];
-      const double s0 = __shfl(av, (tid + 58) & 63, 64);   // a[tid-6]
-      const double a3 = __shfl(av, 3, 64), a4 = __shfl(av, 4, 64), a5 = __shfl(av, 5, 64);
-      double at = av;
-      if (tid >= 6 && tid < 9) at = av + dt * s0;
-      else if (tid == 9) at = av + ((cp * dt) * a3 + (-sp * dt) * a4);
-      else if (tid == 10) at = av + ((sp * dt) * a3 + (cp * dt) * a4);
-      else if (tid == 11) at = av + dt * a5;
-      if (tid < 12) at += qdiag(tid) * (sm[L::XBAR + 12 * t + tid] - sm[L::XREF + 12 * (t - 1) + tid]);
-      av = at;
-      if (tid < 12) sm[L::ADJ + 12 * t + tid] = av;
+      // translational axes and yaw: [[a, b], [b, c]] with p' = p + dt v
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int o = 3 * q;
+        const double aa = s[o], bb = s[o + 1], cc = s[o + 2];
+        s[o + 1] = fma(dt, aa, bb);
+        s[o + 2] = cc + dt * (2.0 * bb + dt * aa);
+      }
+      // roll/pitch block, theta' = theta + D w with D = dt [[c, s], [-s, c]]:
+      //   M' = M + P D,   Qm' = Qm + D'(M + P D) + M' D   (old M in the last term)
+      const double D00 = cp * dt, D01 = sp * dt, D10 = -sp * dt, D11 = cp * dt;
+      const double P00 = s[12], P01 = s[13], P11 = s[14];
+      const double M00 = s[15], M01 = s[16], M10 = s[17], M11 = s[18];
+      const double N00 = M00 + (P00 * D00 + P01 * D10), N01 = M01 + (P00 * D01 + P01 * D11);
+      const double N10 = M10 + (P01 * D00 + P11 * D10), N11 = M11 + (P01 * D01 + P11 * D11);
+      const double A00 = D00 * N00 + D10 * N10, A01 = D00 * N01 + D10 * N11;
+      const double A11 = D01 * N01 + D11 * N11;
+      const double B00 = M00 * D00 + M10 * D10, B01 = M00 * D01 + M10 * D11;
+      const double B11 = M01 * D01 + M11 * D11;
+      s[19] += A00 + B00;
+      s[20] += A01 + B01;
+      s[21] += A11 + B11;
+      s[15] = N00; s[16] = N01; s[17] = N10; s[18] = N11;
+      // + W_{t-1} = Q (diagonal)
+#pragma unroll
+      for (int a3 = 0; a3 < 3; ++a3) {
+        s[3 * a3] += kQ[a3];
+        s[3 * a3 + 2] += kQ[6 + a3];
+      }
+      s[9] += kQ[5]; s[11] += kQ[11];
+      s[12] += kQ[3]; s[14] += kQ[4];
+      s[19] += kQ[9]; s[21] += kQ[10];
+      if (tid == 0)
+#pragma unroll
+        for (int e = 0; e < 22; ++e) sm[L::SS + 22 * (t - 1) + e] = s[e];
     }
   }
   __syncthreads();
+  HMPC_STAMP(3);
 
-  // ---------------- phase 4b: condensed Hessian rows + gradient -------------
+  // ---------------- phase 3: Hessian row (lower part) + gradient ------------
   const int vj = tid / 6, vc = tid - 6 * (tid / 6);   // stage / component of my variable
   const bool active_lane = tid < NV;
   const double ubar_z_alias = (sm[L::CC + N - 1] != 0.0) ? 2.0 * a.m * a.g : 0.0;
@@ -486,153 +578,173 @@ solve_kernel(SolveArgs a) {
   };
   const bool my_fixed = active_lane && is_fixed(vj, vc);
 
-  double Jr[NV];   // row `tid` of H, then L, then J
+  double Rg[NV];   // row `tid` of H (lower part), then the Cholesky trailing row
   double hv = 0.0;
   {
-    double Z[12];
+    const int ii = active_lane ? vj : 0;
+    const int ci = active_lane ? vc : 0;
+    // my impulse b = Bd_i e_c (rows 6..11) and f = S_{i+1} b
+    const double cpi = sm[L::CS + 2 * ii], spi = sm[L::CS + 2 * ii + 1];
+    const double* bwi = sm + L::BW + 18 * ii;
+    double e0[12], f[12];
 #pragma unroll
-    for (int r = 0; r < 12; ++r) Z[r] = 0.0;
-    sfor<0, N>([&](auto ic) __attribute__((always_inline)) {
-      constexpr int i = N - 1 - decltype(ic)::value;
-      if (i < N - 1) {   // Z <- Ad_{i+1}' Z for lanes with j > i
-        const double cp = sm[L::CS + 2 * (i + 1)], sp = sm[L::CS + 2 * (i + 1) + 1];
-        double Zn[12];
+    for (int r = 0; r < 6; ++r) e0[r] = 0.0;
 #pragma unroll
-        for (int r = 0; r < 12; ++r) Zn[r] = Z[r];
+    for (int r = 0; r < 3; ++r) e0[6 + r] = ci < 3 ? bv<VAR>(r, ci, dtm, cpi, spi) : 0.0;
 #pragma unroll
-        for (int r = 6; r < 9; ++r) Zn[r] = Z[r] + dt * Z[r - 6];
-        Zn[9] = Z[9] + ((cp * dt) * Z[3] + (-sp * dt) * Z[4]);
-        Zn[10] = Z[10] + ((sp * dt) * Z[3] + (cp * dt) * Z[4]);
-        Zn[11] = Z[11] + dt * Z[5];
-        const bool upd = vj > i;
+    for (int r = 0; r < 3; ++r) e0[9 + r] = bwi[6 * r + ci];
+    s_times(sm + L::SS + 22 * ii, e0, f);
+    // diagonal block H[v, (i, c2)] = 2 Bd_i[:,c2]' S_{i+1} Bd_i e_c + 2 V_i
+    double hd[6];
 #pragma unroll
-        for (int r = 0; r < 12; ++r) Z[r] = upd ? Zn[r] : Z[r];
+    for (int c2 = 0; c2 < 6; ++c2) {
+      hd[c2] = bd_dot<VAR>(c2, f, bwi, dtm, cpi, spi);
+      if (c2 == ci && ii != N - 1) hd[c2] += 2.0 * kRdiag;
+    }
+    // gradient: h_v = 2 sum_{j >= i} d_{j+1}' e_j, e_j = Phi(j+1, i+1) b
+    double e[12];
+#pragma unroll
+    for (int r = 0; r < 12; ++r) e[r] = 0.0;
+    double hacc = 0.0;
+#pragma unroll 1
+    for (int j = 0; j < N; ++j) {
+      const double cp = sm[L::CS + 2 * j], sp = sm[L::CS + 2 * j + 1];
+      ad_times(e, dt, cp, sp);
+      const bool start = (ii == j);
+#pragma unroll
+      for (int r = 0; r < 12; ++r) e[r] = start ? e0[r] : e[r];
+      double dd = 0.0;
+#pragma unroll
+      for (int r = 0; r < 12; ++r) dd = fma(sm[L::DG + 12 * j + r], e[r], dd);
+      if (ii <= j) hacc += dd;
+    }
+    // lower part, j < i: H[v, (j, c2)] = 2 Bd_j[:,c2]' g_j,
+    // g_i = f, g_j = Ad_{j+1}' g_{j+1}
+    double g[12];
+#pragma unroll
+    for (int r = 0; r < 12; ++r) g[r] = f[r];
+    sfor<0, N>([&](auto jc) __attribute__((always_inline)) {
+      constexpr int j = N - 1 - decltype(jc)::value;
+      const double* smj = sm + opaque_zero();   // keeps this step's loads here
+      if constexpr (j < N - 1) {
+        const double cp1 = smj[L::CS + 2 * (j + 1)], sp1 = smj[L::CS + 2 * (j + 1) + 1];
+        double gn[12];
+#pragma unroll
+        for (int r = 0; r < 12; ++r) gn[r] = g[r];
+        adt_times(gn, dt, cp1, sp1);
+#pragma unroll
+        for (int r = 0; r < 12; ++r) g[r] = (ii > j) ? gn[r] : g[r];
       }
-      {
-        const int oz = opaque_zero();
-        const bool ld = (vj == i) && active_lane;
-        const double* Y = sm + L::YY + 72 * i + oz;
-        const int cc = active_lane ? vc : 0;
-        double yv[12];
-#pragma unroll
-        for (int r = 0; r < 12; ++r) yv[r] = Y[6 * r + cc];   // unconditional gather
-        pin_row(yv);
-#pragma unroll
-        for (int r = 0; r < 12; ++r) Z[r] = ld ? yv[r] : Z[r];
-      }
-      const int oz2 = opaque_zero();
-      const double* bd = sm + L::BD + 36 * i + oz2;
-      const bool row_ok = active_lane && vj >= i && !my_fixed;
-      sfor<0, 6>([&](auto cc2) __attribute__((always_inline)) {
-        constexpr int c2 = decltype(cc2)::value;
-        double acc = 0.0;
-#pragma unroll
-        for (int q = 0; q < 6; ++q) acc += bd[6 * q + c2] * Z[6 + q];
-        acc *= 2.0;
-        if (vj == i && vc == c2) acc += (i == N - 1) ? 0.0 : 2.0 * kRdiag;
-        const bool colfix = is_fixed(i, c2);
-        double val = (row_ok && !colfix) ? acc : 0.0;
-        if (my_fixed && vj == i && vc == c2) val = 1.0;
-        Jr[6 * i + c2] = val;
-        pin(Jr[6 * i + c2]);
+      const double cp = smj[L::CS + 2 * j], sp = smj[L::CS + 2 * j + 1];
+      const double* bw = smj + L::BW + 18 * j;
+      const bool stance_j = smj[L::CC + j] != 0.0;
+      sfor<0, 6>([&](auto c2c) __attribute__((always_inline)) {
+        constexpr int c2 = decltype(c2c)::value;
+        constexpr int w = 6 * j + c2;
+        const double lo = bd_dot<VAR>(c2, g, bw, dtm, cp, sp);
+        double val = (ii > j) ? lo : ((ii == j && c2 <= ci) ? hd[c2] : 0.0);
+        // fixed variables: their row and column of H are those of the identity
+        const bool colfix = (c2 < 3 && !stance_j) || (VAR == 2 && c2 == 1);
+        if (colfix || my_fixed) val = 0.0;
+        if (my_fixed && w == tid) val = 1.0;
+        if (!active_lane) val = 0.0;
+        Rg[w] = val;
+        pin(Rg[w]);
       });
-      pin_row(Z);
     });
-    // gradient h_v = 2 Bd_j' a_{j+1} - 2 V_j ubar_j
     if (active_lane && !my_fixed) {
-      const double* bd = sm + L::BD + 36 * vj;
-      const double* ad = sm + L::ADJ + 12 * (vj + 1);
-      double acc = 0.0;
-#pragma unroll
-      for (int q = 0; q < 6; ++q) acc += bd[6 * q + vc] * ad[6 + q];
       double ub = 0.0;
       if (vc == 2) ub = a.uref_aliased ? ubar_z_alias : ((sm[L::CC + vj] != 0.0) ? 2.0 * a.m * a.g : 0.0);
       const double Vj = (vj == N - 1) ? 0.0 : kRdiag;
-      hv = 2.0 * acc - 2.0 * Vj * ub;
+      hv = 2.0 * hacc - 2.0 * Vj * ub;
     }
   }
-  __syncthreads();   // union A (XLIN/XREF/PF/S/Y/ADJ) is dead from here on
+  __syncthreads();   // union A (XLIN/XREF/PF/S/DG) is dead from here on
+  HMPC_STAMP(4);
 
   int status = ST_SOLVED;
 
-  // ---------------- phase 5: Cholesky (right-looking, one column per step) --
+  // ---------------- phase 4: Cholesky ---------------------------------------
+  // Register j of the row always holds column j.  Columns go in blocks of 8:
+  // one runtime loop of 8 steps per block, whose body updates registers
+  // [8bb, NV) -- the same code for all 8 steps, so the kernel keeps a small
+  // instruction footprint.  Step k publishes column k (lanes >= k) through
+  // LDS; registers of already-eliminated columns take harmless garbage.
   {
-    double* Lp = sm + L::LP;
+    double* Lc = sm + L::LC;
     double* invd = sm + L::INVD;
-    sfor<0, NV>([&](auto kc) __attribute__((always_inline)) {
-      constexpr int k = decltype(kc)::value;
-      double* col = sm + L::COL + (k & 1) * NT;
-      col[tid] = Jr[k];
-      __syncthreads();
-      col += opaque_zero();
-      const double piv = col[k];
-      const double sq = sqrt(piv > 0.0 ? piv : 1.0);
-      if (!(piv > 0.0)) status = ST_NUMERICAL;
-      const double rs = 1.0 / sq;
-      const double tk = Jr[k] * (rs * rs);
-      row_axpy<k + 1, NV, 8>(Jr, -tk, col);
-      const double lik = Jr[k] * rs;
-      Jr[k] = lik;
-      const bool wr = tid >= k && tid < NV;
-      Lp[wr ? loff(tid) + k : L::LPS - NT + tid] = lik;   // branch-free (pad slots)
-      if (tid == k) invd[k] = rs;
-      pin_row(Jr);
+    sfor<0, (NV + 7) / 8>([&](auto bc) __attribute__((always_inline)) {
+      constexpr int bb = decltype(bc)::value;
+      constexpr int J0 = 8 * bb;
+      constexpr int KEND = (J0 + 8 < NV) ? J0 + 8 : NV;
+      constexpr int NCH = (NV - J0 + 7) / 8;   // chunks of 8 registers in [J0, NV)
+#pragma unroll 1
+      for (int k = J0; k < KEND; ++k) {
+        const int kk = k - J0;
+        double* col = sm + L::COLB + (k & 1) * (NT + 8);
+        // mine = Rg[k] = A[tid][k] (current).  The pins hide the select chain
+        // from the pattern that would turn it into a dynamic index (and the
+        // whole row into scratch).
+        double mine = Rg[J0];
+        pin(mine);
+        sfor<1, KEND - J0>([&](auto jc) __attribute__((always_inline)) {
+          constexpr int jj = decltype(jc)::value;
+          double c = Rg[J0 + jj];
+          pin(c);
+          mine = (kk == jj) ? c : mine;
+        });
+        col[tid] = (tid >= k && tid < NV) ? mine : 0.0;
+        B::sync();
+        const double piv = (W == 1) ? rdlane(mine, k) : col[k];
+        const double pv = piv > 0.0 ? piv : 1.0;
+        if (!(piv > 0.0)) status = ST_NUMERICAL;
+        const double rs = 1.0 / sqrt(pv);
+        const double lik = mine * rs;
+        if (tid >= k && tid < NV) Lc[L::cb(k) + tid - k] = lik;
+        if (tid == k) invd[k] = rs;
+        const double nt = (tid > k && tid < NV) ? -lik * rs : 0.0;
+        // Rg[j] += nt * col[j], j in [J0, NV): 16-byte loads, one chunk ahead
+        const double2* c2 = reinterpret_cast<const double2*>(col + J0);
+        double2 buf[2][4];
+        auto load = [&](auto chc) __attribute__((always_inline)) {
+          constexpr int ch = decltype(chc)::value;
+          const double2* pp = c2 + 4 * ch + opaque_zero();
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (J0 + 8 * ch + 2 * i < NV) buf[ch & 1][i] = pp[i];
+        };
+        load(std::integral_constant<int, 0>{});
+        sfor<0, NCH>([&](auto chc) __attribute__((always_inline)) {
+          constexpr int ch = decltype(chc)::value;
+          if constexpr (ch + 1 < NCH) load(std::integral_constant<int, ch + 1>{});
+          sfor<0, 8>([&](auto ic) __attribute__((always_inline)) {
+            constexpr int i = decltype(ic)::value;
+            constexpr int j = J0 + 8 * ch + i;
+            if constexpr (j < NV) {
+              const double cv = (i & 1) ? buf[ch & 1][i / 2].y : buf[ch & 1][i / 2].x;
+              Rg[j] = fma(nt, cv, Rg[j]);
+              pin(Rg[j]);
+            }
+          });
+        });
+      }
     });
     __syncthreads();
   }
+  HMPC_STAMP(5);
 
-  // ---------------- phase 7 (first): v0 = -L^-T L^-1 h -----------------------
+  const double* Lc = sm + L::LC;
+  const double* invd = sm + L::INVD;
+
+  // ---------------- phase 5: v0 = -L^-T L^-1 h -------------------------------
   double v = 0.0;
   {
-    const double* Lp = sm + L::LP;
-    const double* invd = sm + L::INVD;
-    double acc = hv, yv = 0.0;
-    for (int s = 0; s < NV; ++s) {
-      const double ys = B::bcast(acc, s, red) * invd[s];
-      const int cidx = tid > s ? tid : s;   // keep the address inside the array
-      const double lis = Lp[loff(cidx < NV ? cidx : NV - 1) + s];
-      if (tid > s) acc = fma(-lis, ys, acc);
-      if (tid == s) yv = ys;
-    }
-    acc = yv;
-    for (int s = NV - 1; s >= 0; --s) {
-      const double vs = B::bcast(acc, s, red) * invd[s];
-      const double lsi = Lp[loff(s) + (tid < s ? tid : 0)];
-      if (tid < s) acc = fma(-lsi, vs, acc);
-      if (tid == s) v = -vs;
-    }
+    const double y = tri_fwd<N>(-hv, 0, Lc, invd, red);
+    v = tri_bwd<N>(y, Lc, invd, red);
   }
+  HMPC_STAMP(6);
 
-  // ---------------- phase 6: J = L^-T, row `tid` of J in registers ----------
-  {
-    const double* Lp = sm + L::LP;
-    const double* invd = sm + L::INVD;
-    sfor<0, NV>([&](auto rc) __attribute__((always_inline)) {
-      constexpr int r = decltype(rc)::value;
-      double acc0 = (tid == r) ? 1.0 : 0.0, acc1 = 0.0, acc2 = 0.0, acc3 = 0.0;
-      const double* Lr = Lp + loff(r) + opaque_zero();
-      sfor<0, r / 4>([&](auto sc) __attribute__((always_inline)) {
-        constexpr int s = 4 * decltype(sc)::value;
-        if constexpr ((s % 8) == 0) {
-          Lr += opaque_zero();
-          pin(acc0); pin(acc1); pin(acc2); pin(acc3);
-        }
-        acc0 = fma(-Lr[s], Jr[s], acc0);
-        acc1 = fma(-Lr[s + 1], Jr[s + 1], acc1);
-        acc2 = fma(-Lr[s + 2], Jr[s + 2], acc2);
-        acc3 = fma(-Lr[s + 3], Jr[s + 3], acc3);
-      });
-      sfor<(r / 4) * 4, r>([&](auto sc) __attribute__((always_inline)) {
-        constexpr int s = decltype(sc)::value;
-        acc0 = fma(-Lr[s], Jr[s], acc0);
-      });
-      Jr[r] = ((acc0 + acc1) + (acc2 + acc3)) * invd[r];
-      pin(Jr[r]);
-    });
-  }
-  __syncthreads();   // L is dead: its LDS becomes R
-
-  // ---------------- phase 8: Goldfarb-Idnani dual active set ----------------
+  // ---------------- phase 6: Goldfarb-Idnani, range-space form --------------
   // Constraints owned by lane v (id = 4 v + slot), all as n'v >= b:
   //   c in 3..5 : slot0  v >= -lim,  slot1 -v >= -lim          (:123-128)
   //   c == 3    : slot2  z_k >= 0.1, k = stage, 2 <= k <= N-1  (:129)
@@ -640,11 +752,13 @@ solve_kernel(SolveArgs a) {
   //   c in 0..1 : slot0 -f + mu fz >= 0, slot1 f + mu fz >= 0   (:141-144)
   //   (stance only for c <= 2; 2f has no fy rows)
   int iters = 0;
-  const double zmin_gap_k0 = sm[L::XIN + 2] - kZmin;       // z_0 row: constant
-  const double zmin_gap_k1 = sm[L::XBAR + 12 + 2] - kZmin;  // z_1 row: constant
+  const double zmin_gap_k0 = sm[L::XIN + 2] - kZmin;    // z_0 row: constant
+  const double zmin_gap_k1 = sm[L::ZB + 1] - kZmin;     // z_1 row: constant
   if (zmin_gap_k0 < -kTol || zmin_gap_k1 < -kTol) status = ST_INFEAS;
+  // coefficient of fz_j in z_k (j <= k-2): dt * (dt/m) * (k-1-j), stance only
+  // (Bd[8][2] = dt/m in both variants)
+  const double zc = dt * dtm;
 
-  // my constraint slots: number, and the z-row norm for lanes (k,3)
   const bool stance_me = active_lane && vc <= 2 && sm[L::CC + vj] != 0.0;
   int nslots = 0;
   if (active_lane) {
@@ -656,7 +770,7 @@ solve_kernel(SolveArgs a) {
     double s2 = 0.0;
     for (int j = 0; j <= vj - 2; ++j) {
       if (sm[L::CC + j] != 0.0) {
-        double cz = dt * sm[L::BD + 36 * j + 2 * 6 + 2] * (double)(vj - 1 - j);
+        const double cz = zc * (double)(vj - 1 - j);
         s2 += cz * cz;
       }
     }
@@ -665,14 +779,16 @@ solve_kernel(SolveArgs a) {
   const double fric_norm = sqrt(1.0 + mu * mu);
   int actmask = 0;
 
-  double* Rm = sm + L::LP;   // packed upper, column k at loff(k)
+  double* Rm = sm + L::RM;   // packed upper, column k at loff(k)
   double* ua = sm + L::UA;
-  double* rv = sm + L::RV;
   int* act = reinterpret_cast<int*>(sm + L::ACT);
-  double* dz = sm + L::DZ;
-  double* xs = sm + L::XS;
-  double* slot = sm + L::SLOT;
+  double* cbv = sm + L::CB;
+  double* gv = sm + L::GV;
   double* sdg = sm + L::SD;
+  double* xs = sm + L::XS;
+  double Qw[QMAX];   // row `tid` of the orthonormal basis of L^-1 N_A
+#pragma unroll
+  for (int l = 0; l < QMAX; ++l) Qw[l] = 0.0;
   int q = 0;
   const int max_iter = 4 * NV + 50;
 
@@ -686,7 +802,7 @@ solve_kernel(SolveArgs a) {
       // z-row of stage oj over fz_j, j <= oj-2
       const int ij = i / 6, ic = i - 6 * ij;
       if (ic != 2 || ij > oj - 2 || sm[L::CC + ij] == 0.0) return 0.0;
-      return dt * sm[L::BD + 36 * ij + 2 * 6 + 2] * (double)(oj - 1 - ij);
+      return zc * (double)(oj - 1 - ij);
     }
     if (oc == 2) return i == o ? (sl == 0 ? 1.0 : -1.0) : 0.0;
     if (i == o) return sl == 0 ? -1.0 : 1.0;
@@ -697,7 +813,7 @@ solve_kernel(SolveArgs a) {
     const int o = id >> 2, sl = id & 3, oj = o / 6, oc = o - 6 * oj;
     if (oc >= 3) {
       if (sl < 2) return -tau_lim(oc);
-      return kZmin - sm[L::XBAR + 12 * oj + 2];
+      return kZmin - sm[L::ZB + oj];
     }
     if (oc == 2) return sl == 0 ? 0.0 : -kFzMax;
     return 0.0;
@@ -707,7 +823,7 @@ solve_kernel(SolveArgs a) {
   while (!done) {
     // ---- slacks of my constraints; pick the most violated ----
     xs[tid] = v;
-    __syncthreads();
+    B::sync();
     double best = INFINITY;
     int bid = 0x7fffffff;
     for (int sl = 0; sl < nslots; ++sl) {
@@ -718,10 +834,9 @@ solve_kernel(SolveArgs a) {
           s = (sl == 0 ? v : -v) + tau_lim(vc);
           nrm = 1.0;
         } else {
-          double z = sm[L::XBAR + 12 * vj + 2];
+          double z = sm[L::ZB + vj];
           for (int j = 0; j <= vj - 2; ++j)
-            if (sm[L::CC + j] != 0.0)
-              z += dt * sm[L::BD + 36 * j + 14] * (double)(vj - 1 - j) * xs[6 * j + 2];
+            if (sm[L::CC + j] != 0.0) z += zc * (double)(vj - 1 - j) * xs[6 * j + 2];
           s = z - kZmin;
           nrm = znorm;
         }
@@ -740,49 +855,41 @@ solve_kernel(SolveArgs a) {
     }
     B::argmin(best, bid, red);
     if (!(best < -kTol)) break;   // primal feasible: optimal
-    const int p = bid;
+    const int p = uni(bid);
     const double bp = rhs_of(p);
     const double np_me = coef_of(p, tid);
     double u_plus = 0.0;
+    // w = L^-1 n_p, from the first nonzero of n_p on
+    const int s0 = B::first(np_me != 0.0, red);
+    const double wfull = tri_fwd<N>(np_me, s0 < 0 ? NV : s0, Lc, invd, red);
+    const double wnorm2 = B::sum(wfull * wfull, red);
 
     // ---- inner loop: step towards satisfying constraint p ----
     while (true) {
       if (++iters > max_iter) { status = ST_MAXIT; done = true; break; }
-      // d = J' n_p  (lane j gets d_j) through NSLOT row slots
-      int rk, cnt;
-      const bool nzf = np_me != 0.0;
-      B::rank(nzf, rk, cnt, red);
-      double dj = 0.0;
-      for (int base = 0; base < cnt; base += L::NSLOT) {
-        {
-          // branch-free: lanes without a slot write into the pad row
-          const bool mine = nzf && rk >= base && rk < base + L::NSLOT;
-          double* sr = slot + (mine ? (rk - base) * NV : L::NSLOT * NV);
-          sfor<0, NV>([&](auto jc) __attribute__((always_inline)) {
-            constexpr int j = decltype(jc)::value;
-            double prod = np_me * Jr[j];
-            pin(prod);
-            sr[j] = prod;
-          });
-        }
-        __syncthreads();
-        const int ns = (cnt - base) < L::NSLOT ? (cnt - base) : L::NSLOT;
-        if (tid < NV)
-          for (int s = 0; s < ns; ++s) dj += slot[s * NV + tid];
-        __syncthreads();
+      const int qu = uni(q);
+      // w_perp = (I - Qw Qw') w and c = Qw' w by modified Gram-Schmidt; a
+      // second pass when the first one cancels more than half the norm
+      double wp = wfull, zn = wnorm2;
+#pragma unroll 1
+      for (int pass = 0; pass < 2 && qu > 0; ++pass) {
+        ladder<0, QMAX>(qu, [&](auto lc) __attribute__((always_inline)) {
+          constexpr int l = decltype(lc)::value;
+          const double cl = B::sum(Qw[l] * wp, red);
+          wp = fma(-cl, Qw[l], wp);
+          if (tid == 0) cbv[l] = (pass == 0) ? cl : cbv[l] + cl;
+        });
+        const double n2 = B::sum(wp * wp, red);
+        const bool enough = n2 > 0.25 * zn;
+        zn = n2;
+        if (enough) break;
       }
-      // z = J_2 d_2, |d_2|^2
-      const bool in2 = tid >= q && tid < NV;
-      dz[tid] = in2 ? dj : 0.0;
-      const double zn = B::sum(in2 ? dj * dj : 0.0, red);
-      __syncthreads();
-      double zi = 0.0;
-      {
-        zi = row_dot<0, NV, 8>(Jr, dz);
-      }
-      // r = R^-1 d_1 (lanes l < q), back substitution
-      double rcur = tid < q ? dj : 0.0, rmine = 0.0;
-      for (int l = q - 1; l >= 0; --l) {
+      B::sync();
+      // primal direction z = L^-T w_perp (lane v gets z_v)
+      const double zi = tri_bwd<N>(wp, Lc, invd, red);
+      // dual direction r = R^-1 c (lanes l < q), back substitution
+      double rcur = tid < qu ? cbv[tid] : 0.0, rmine = 0.0;
+      for (int l = qu - 1; l >= 0; --l) {
         const double rl = B::bcast(rcur, l, red) / Rm[loff(l) + l];
         if (tid == l) rmine = rl;
         if (tid < l) rcur = fma(-Rm[loff(l) + tid], rl, rcur);
@@ -790,135 +897,154 @@ solve_kernel(SolveArgs a) {
       // partial step length t1 (drop candidate)
       double t1 = INFINITY;
       int kdrop = 0x7fffffff;
-      if (tid < q && rmine > 0.0) { t1 = ua[tid] / rmine; kdrop = tid; }
+      if (tid < qu && rmine > 0.0) { t1 = ua[tid] / rmine; kdrop = tid; }
       B::argmin(t1, kdrop, red);
-      // full step length t2
+      // full step length t2 (n_p' z = |w_perp|^2)
       const double sp_ = B::sum(np_me * v, red) - bp;
-      const bool has_z = zn > 1e-30;
+      const bool has_z = zn > 1e-24 * wnorm2;
       const double t2 = has_z ? -sp_ / zn : INFINITY;
       const double t = t1 < t2 ? t1 : t2;
       if (!(t < INFINITY)) { status = ST_INFEAS; done = true; break; }
       if (has_z) v = fma(t, zi, v);
-      if (tid < q) ua[tid] -= t * rmine;
+      if (tid < qu) ua[tid] -= t * rmine;
       u_plus += t;
-      __syncthreads();
+      B::sync();
       if (has_z && t == t2) {
-        // ---- add p: Householder reflection on d_2 ----
-        const double dq = B::bcast(dj, q, red);
-        const double nrm = sqrt(zn);
-        const double alpha = dq > 0.0 ? -nrm : nrm;
-        const double ww = (zn - dq * dq) + (dq - alpha) * (dq - alpha);
-        dz[tid] = in2 ? (tid == q ? dj - alpha : dj) : 0.0;
-        if (tid < q) Rm[loff(q) + tid] = dj;
-        if (tid == q) Rm[loff(q) + q] = alpha;
-        if (tid == 0) { act[q] = p; ua[q] = u_plus; }
+        // ---- add p: new basis column w_perp / |w_perp|, R column [c; rho] ----
+        if (qu >= QMAX) { status = ST_NUMERICAL; done = true; break; }
+        const double rho = sqrt(zn);
+        const double qn = wp / rho;
+        // (selects over every register, not a branch per index: branches that
+        // store to different elements get merged into one dynamically
+        // indexed store, and the array lands in scratch)
+#pragma unroll
+        for (int l = 0; l < QMAX; ++l) Qw[l] = (l == qu) ? qn : Qw[l];
+        if (tid < qu) Rm[loff(qu) + tid] = cbv[tid];
+        if (tid == qu) Rm[loff(qu) + qu] = rho;
+        if (tid == 0) { act[qu] = p; ua[qu] = u_plus; }
         if (tid == (p >> 2)) actmask |= 1 << (p & 3);
-        __syncthreads();
-        if (ww > 0.0) {
-          const double f = row_dot<0, NV, 8>(Jr, dz) * (2.0 / ww);
-          row_axpy<0, NV, 8>(Jr, -f, dz);
-        }
-        ++q;
-        __syncthreads();
+        q = qu + 1;
+        B::sync();
         break;
       }
       // ---- drop active constraint kdrop ----
       {
-        const int k = kdrop;
+        const int k = uni(kdrop);
         const int idk = act[k];
         if (tid == (idk >> 2)) actmask &= ~(1 << (idk & 3));
         // shift R columns k+1..q-1 left; remember the subdiagonals
-        for (int m = k; m + 1 < q; ++m) {
+        for (int m = k; m + 1 < qu; ++m) {
           double val = 0.0;
           if (tid <= m + 1) val = Rm[loff(m + 1) + tid];
-          __syncthreads();
+          B::sync();
           if (tid <= m) Rm[loff(m) + tid] = val;
           if (tid == m + 1) sdg[m] = val;
-          __syncthreads();
+          B::sync();
         }
         // shift the active list and multipliers
         {
           int an = 0;
           double un = 0.0;
-          if (tid >= k && tid + 1 < q) { an = act[tid + 1]; un = ua[tid + 1]; }
-          __syncthreads();
-          if (tid >= k && tid + 1 < q) { act[tid] = an; ua[tid] = un; }
-          __syncthreads();
+          if (tid >= k && tid + 1 < qu) { an = act[tid + 1]; un = ua[tid + 1]; }
+          B::sync();
+          if (tid >= k && tid + 1 < qu) { act[tid] = an; ua[tid] = un; }
+          B::sync();
         }
         // Givens to restore the triangle: rows (l, l+1), l = k..q-2
-        for (int l = k; l + 1 < q; ++l) {
+        for (int l = k; l + 1 < qu; ++l) {
           const double aa = Rm[loff(l) + l], bb = sdg[l];
           const double hh = sqrt(aa * aa + bb * bb);
           const double cg = aa / hh, sg = bb / hh;
-          __syncthreads();
-          if (tid == l) Rm[loff(l) + l] = hh;
+          B::sync();
+          if (tid == l) { Rm[loff(l) + l] = hh; gv[2 * l] = cg; gv[2 * l + 1] = sg; }
           const int mcol = tid;   // columns m > l hold rows l, l+1
-          if (mcol > l && mcol + 1 < q) {
+          if (mcol > l && mcol + 1 < qu) {
             const double rl = Rm[loff(mcol) + l], rl1 = Rm[loff(mcol) + l + 1];
             Rm[loff(mcol) + l] = cg * rl + sg * rl1;
             Rm[loff(mcol) + l + 1] = -sg * rl + cg * rl1;
           }
-          sfor<0, NV - 1>([&](auto jc) __attribute__((always_inline)) {
-            constexpr int jj = decltype(jc)::value;
-            if (jj == l) {
-              const double x0 = Jr[jj], x1 = Jr[jj + 1];
-              Jr[jj] = cg * x0 + sg * x1;
-              Jr[jj + 1] = -sg * x0 + cg * x1;
-            }
-          });
-          pin_row(Jr);
-          __syncthreads();
+          B::sync();
         }
-        --q;
-        __syncthreads();
+        // the same rotations on the basis columns (Qw <- Qw G')
+#pragma unroll
+        for (int l = 0; l + 1 < QMAX; ++l) {
+          const bool rot = l >= k && l + 1 < qu;
+          const int lg = rot ? l : 0;
+          const double cg = gv[2 * lg], sg = gv[2 * lg + 1];
+          const double x0 = Qw[l], x1 = Qw[l + 1];
+          Qw[l] = rot ? cg * x0 + sg * x1 : x0;
+          Qw[l + 1] = rot ? -sg * x0 + cg * x1 : x1;
+        }
+#pragma unroll
+        for (int l = 0; l < QMAX; ++l) Qw[l] = (l == qu - 1) ? 0.0 : Qw[l];
+        q = qu - 1;
+        B::sync();
       }
     }
   }
+  HMPC_STAMP(7);
 
-  // ---------------- phase 9: outputs ----------------------------------------
+  // ---------------- phase 7: outputs ----------------------------------------
   if (active_lane) a.u[b * NV + tid] = v;
   xs[tid] = v;
-  __syncthreads();
+  __syncthreads();   // L is dead: XO aliases it
   {
-    double* xo = sm + L::XOUT;
-    double xv = tid < 12 ? sm[L::XIN + tid] : 0.0;
-    if (tid < 12) xo[tid] = xv;
-    double objp = 0.0;
+    double* xo = sm + L::XO;
+    double x[12];
+#pragma unroll
+    for (int r = 0; r < 12; ++r) x[r] = sm[L::XIN + r];
+    if (tid < 12) xo[tid] = sm[L::XIN + tid];
+    double objv = 0.0;
     const double* xr = a.x_ref + b * 12 * N;
+#pragma unroll 1
     for (int k = 0; k < N; ++k) {
       const double cp = sm[L::CS + 2 * k], sp = sm[L::CS + 2 * k + 1];
-      const double vsrc = __shfl(xv, (tid + 6) & 63, 64);
-      const double w0 = __shfl(xv, 9, 64), w1 = __shfl(xv, 10, 64), w2 = __shfl(xv, 11, 64);
-      double nx = xv;
-      if (tid < 3) nx = xv + dt * vsrc;
-      else if (tid == 3) nx = xv + ((cp * dt) * w0 + (sp * dt) * w1);
-      else if (tid == 4) nx = xv + ((-sp * dt) * w0 + (cp * dt) * w1);
-      else if (tid == 5) nx = xv + dt * w2;
-      else if (tid >= 6 && tid < 12) {
-        const double* bd = sm + L::BD + 36 * k + 6 * (tid - 6);
-        double bu = 0.0;
+      const double* bw = sm + L::BW + 18 * k;
+      double u[6];
 #pragma unroll
-        for (int c = 0; c < 6; ++c) bu += bd[c] * xs[6 * k + c];
-        nx = xv + bu;
-        if (tid == 8) nx += -a.g * dt;
+      for (int c = 0; c < 6; ++c) u[c] = xs[6 * k + c];
+      ad_times(x, dt, cp, sp);
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        double acc = 0.0;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) acc = fma(bv<VAR>(r, c, dtm, cp, sp), u[c], acc);
+        x[6 + r] += acc;
+        double acw = 0.0;
+#pragma unroll
+        for (int c = 0; c < 6; ++c) acw = fma(bw[6 * r + c], u[c], acw);
+        x[9 + r] += acw;
       }
-      xv = nx;
-      if (tid < 12) {
-        xo[12 * (k + 1) + tid] = xv;
-        const double e = xv - xr[12 * k + tid];
-        objp += (k == N - 1 ? kTermQ : 1.0) * qdiag(tid) * e * e;
+      x[8] += -a.g * dt;
+      const double kf = (k == N - 1) ? kTermQ : 1.0;
+#pragma unroll
+      for (int r = 0; r < 12; ++r) {
+        const double e = x[r] - xr[12 * k + r];
+        objv = fma(kf * kQ[r] * e, e, objv);
       }
-      if (tid < 6 && k < N - 1) {
-        double ub = 0.0;
-        if (tid == 2) ub = a.uref_aliased ? ubar_z_alias : ((sm[L::CC + k] != 0.0) ? 2.0 * a.m * a.g : 0.0);
-        const double du = xs[6 * k + tid] - ub;
-        objp += kRdiag * du * du;
+      if (k < N - 1) {
+        const double ub = a.uref_aliased ? ubar_z_alias
+                                         : ((sm[L::CC + k] != 0.0) ? 2.0 * a.m * a.g : 0.0);
+#pragma unroll
+        for (int c = 0; c < 6; ++c) {
+          const double du = u[c] - (c == 2 ? ub : 0.0);
+          objv = fma(kRdiag * du, du, objv);
+        }
       }
+      if (tid == 0)
+#pragma unroll
+        for (int r = 0; r < 12; ++r) xo[12 * (k + 1) + r] = x[r];
     }
-    const double objv = B::sum(objp, red);
     __syncthreads();
+#ifndef HMPC_STAMPS
     if (a.x)
       for (int i = tid; i < 12 * (N + 1); i += NT) a.x[b * 12 * (N + 1) + i] = xo[i];
+#else
+    HMPC_STAMP(8);
+    if (a.x && tid == 0)
+      for (int i = 0; i < 12; ++i)
+        reinterpret_cast<long long*>(a.x)[b * 12 * (N + 1) + i] = stamp_[i];
+#endif
     if (tid == 0) {
       if (a.obj) a.obj[b] = objv;
       a.status[b] = status;

@@ -1,0 +1,53 @@
+"""Per-phase cycle breakdown of the solve kernel (diagnostic build).
+
+Build:  OUT=libhmpc_stamps.so BDIR=build_stamps HORIZONS=10 \
+        hopper-mpc-inertial_amd/build.sh -DHMPC_STAMPS
+Run:    HMPC_LIB=hopper-mpc-inertial_amd/libhmpc_stamps.so python tools/phase_stamps.py
+The stamped kernel writes s_memtime values over each instance's x* row.
+"""
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, 'hopper-mpc-inertial_amd'))
+sys.path.insert(0, ROOT)
+import hmpc  # noqa: E402
+import hmpc_plan  # noqa: E402
+from oracle import hmpc_oracle as ho  # noqa: E402
+
+NAMES = ['load', 'gen_dt_dynamics', 'uniform_sweeps', 'hessian_rows', 'cholesky', 'unconstrained', 'active_set', 'outputs']
+         'unconstr_solve', 'J=L^-T', 'active_set', 'outputs']
+
+
+def main():
+    N = int(os.environ.get('N', '10'))
+    B = int(os.environ.get('B', '65536'))
+    var = os.environ.get('VARIANT', '3f')
+    inst = hmpc_plan.sample_instances(B, N, curve=True, seed=2024)
+    d = {k: torch.from_numpy(np.ascontiguousarray(inst[k])).cuda()
+         for k in ('x_in', 'x_lin', 'x_ref', 'pf', 'C', 'mu')}
+    c = ho.runner_constants()
+    ctx = hmpc.Context(var, N, t=c['t'], m=c['m'], g=c['g'], mu=1.0, Jinv=c['Jinv'], rh=c['rh'])
+    for _ in range(3):
+        out = ctx.solve_device(d['x_in'], d['x_lin'], d['x_ref'], d['pf'], d['C'], mu=d['mu'])
+    torch.cuda.synchronize()
+    st = out['x'].view(torch.int64).reshape(B, -1)[:, :len(NAMES) + 1].cpu().numpy()
+    dur = np.diff(st, axis=1)
+    tot = st[:, len(NAMES)] - st[:, 0]
+    res = {n: float(dur[:, i].mean()) for i, n in enumerate(NAMES)}
+    res['total_mean'] = float(tot.mean())
+    res['total_p50'] = float(np.median(tot))
+    res['total_max'] = float(tot.max())
+    wall = st[:, len(NAMES)].max() - st[:, 0].min()
+    res['wall_cycles'] = float(wall)
+    res['mean_in_flight'] = float(tot.sum() / wall)
+    res['iters_mean'] = float(out['iters'].float().mean())
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == '__main__':
+    main()
