@@ -93,6 +93,40 @@ __device__ __forceinline__ int opaque_zero() {
   return z;
 }
 
+// 1/sqrt(p) to ~1 ulp without the IEEE sqrt + divide sequences (two dependent
+// chains of ~15 f64 ops each): hardware v_rsq_f64 estimate, then one
+// third-order correction y (1 + e/2 + 3e^2/8), e = 1 - p y^2.
+__device__ __forceinline__ double rsq_nr(double p) {
+  const double y = __builtin_amdgcn_rsq(p);
+  const double e = fma(-(p * y), y, 1.0);
+  return fma(y * e, fma(0.375, e, 0.5), y);
+}
+
+// LDS loads the scheduler cannot move.  hipcc sinks prefetches next to their
+// use and then waits with lgkmcnt(0); these are issued where they stand, and
+// the value is valid only after the matching lds_wait (s_waitcnt lgkmcnt(n),
+// n = LDS instructions issued after the load), which also ties the registers
+// so nothing reads them earlier.
+typedef double dbl2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
+  return (unsigned)(uintptr_t)p;   // low 32 bits of the flat address = LDS offset
+}
+template <int OFF>
+__device__ __forceinline__ void lds_ld128(dbl2& v, unsigned base) {
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(base), "i"(OFF) : "memory");
+}
+__device__ __forceinline__ void lds_ld64(double& v, unsigned addr) {
+  asm volatile("ds_read_b64 %0, %1" : "=v"(v) : "v"(addr) : "memory");
+}
+template <int CNT>
+__device__ __forceinline__ void lds_wait(dbl2& a, dbl2& b, dbl2& c, dbl2& d) {
+  asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(a), "+v"(b), "+v"(c), "+v"(d) : "i"(CNT));
+}
+template <int CNT>
+__device__ __forceinline__ void lds_wait(double& a) {
+  asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(a) : "i"(CNT));
+}
+
 // ----------------------------------------------------------------------------
 // constants of Mpc.__init__ / build_qp (src/mpc_cvx_euler_3f.py:20,35,37,113-129)
 // ----------------------------------------------------------------------------
@@ -225,8 +259,8 @@ struct Lay {
   static constexpr int ZB = BW + 18 * N;           // [N+1] free-response heights
   static constexpr int XS = ZB + e2(N + 1);        // [NT] primal broadcast
   static constexpr int RED = XS + NT;              // [16]
-  static constexpr int INVD = RED + 16;            // [NV] 1 / L_kk
-  static constexpr int UA = INVD + e2(NV);         // [QMAX] active multipliers
+  static constexpr int ZR = RED + 16;              // [2] a 0.0 for masked lanes' loads
+  static constexpr int UA = ZR + 2;                // [QMAX] active multipliers
   static constexpr int ACT = UA + QMAX;            // [QMAX] active ids (int)
   static constexpr int CB = ACT + QMAX;            // [QMAX] c = Qw' w
   static constexpr int GV = CB + QMAX;             // [QMAX][2] Givens of a drop
@@ -240,9 +274,10 @@ struct Lay {
   static constexpr int XREF = PF + e2(3 * N);      // [N][12]
   static constexpr int SS = XREF + 12 * N;         // [N][22]  S_{t}, t = 1..N
   static constexpr int DG = SS + NS * N;           // [N][12]  d_t, t = 1..N
-  static constexpr int ENDA = DG + 12 * N;
+  static constexpr int AJ = DG + 12 * N;           // [N][6]   adjoint a_t rows 6..11, t = 1..N
+  static constexpr int ENDA = AJ + 6 * N;
   // union B (phases 4-7)
-  static constexpr int LC = U0;                    // L, column-major packed
+  static constexpr int LC = U0;                    // M = L diag(L)^-1, column-major packed
   static constexpr int XO = U0;                    // x* staging (after L is dead)
   static constexpr int ENDB = LC + e2(LCN);
   static constexpr int TOTAL = ENDA > ENDB ? ENDA : ENDB;
@@ -323,43 +358,121 @@ __device__ __forceinline__ double bd_dot(int c2, const double (&y)[12], const do
 }
 
 // ----------------------------------------------------------------------------
-// triangular sweeps with L column-major packed in LDS (lane v = row v)
+// triangular sweeps.  The factor is kept as the unit lower M = L diag(L)^-1:
+// row tid of M in lane tid's registers (Mr, after the Cholesky), and a
+// column-major packed copy in LDS with 1/L_kk in the (unit) diagonal slot of
+// column k.  L^-1 b = diag(1/L) M^-1 b and L^-T b = M^-T (diag(1/L) b): one
+// step's dependent chain is just readlane -> fma.
 // ----------------------------------------------------------------------------
-// y = L^-1 b (lane v holds b_v); rows before s0 are zero
+// y = L^-1 b (lane v holds b_v), M from registers, fully unrolled.
+// Mr[s] = M[tid][s] below the diagonal, 1/L_ss on it (the stale update of
+// the finished lane is harmless) and 0 above.
 template <int N>
-__device__ __forceinline__ double tri_fwd(double acc, int s0, const double* Lc,
-                                          const double* invd, double* red) {
-  using L = Lay<N>;
-  constexpr int NV = L::NV;
-  const int tid = threadIdx.x;
-  double y = 0.0;
-#pragma unroll 1
-  for (int s = s0; s < NV; ++s) {
-    const bool below = tid > s && tid < NV;
-    double l = Lc[L::cb(s) + (below ? tid - s : 0)];
-    const double ys = Blk<L::W>::bcast(acc, s, red) * invd[s];
-    if (tid == s) y = ys;
-    if (!below) l = 0.0;
-    acc = fma(-l, ys, acc);
-  }
-  return y;
-}
-// z = L^-T b (lane v holds b_v)
-template <int N>
-__device__ __forceinline__ double tri_bwd(double acc, const double* Lc, const double* invd,
+__device__ __forceinline__ double tri_fwd(double acc, const double (&Mr)[6 * N], double dinv,
                                           double* red) {
   using L = Lay<N>;
   constexpr int NV = L::NV;
   const int tid = threadIdx.x;
-  double z = 0.0;
+  double yp = 0.0;
+  sfor<0, NV>([&](auto sc) __attribute__((always_inline)) {
+    constexpr int s = decltype(sc)::value;
+    const double ys = Blk<L::W>::bcast(acc, s, red);
+    if (tid == s) yp = ys;
+    acc = fma(-Mr[s], ys, acc);
+  });
+  return yp * dinv;
+}
+// The same sweep from the LDS copy (the active-set phase, where the
+// registers hold the Gram-Schmidt basis instead): loads of step s+4 are
+// issued at step s (a 4-deep ring of hand-counted loads).
+template <int N>
+__device__ __forceinline__ double tri_fwd_lds(double acc, const double* Mc, const double* zero,
+                                              double dinv, double* red) {
+  using L = Lay<N>;
+  constexpr int NV = L::NV;
+  constexpr int SEND = (NV + 3) & ~3;   // padded (steps >= NV are no-ops)
+  const int tid = threadIdx.x;
+  double yp = 0.0;
+  if constexpr (L::W == 1) {
+    // M[tid][s] for tid > s sits at Mc[cb(s) + tid - s]; other lanes read a 0
+    const unsigned base = lds_addr(Mc + tid), zaddr = lds_addr(zero);
+    auto addr = [&](int s) -> unsigned {
+      return (tid > s && tid < NV && s < NV) ? base + 8u * (unsigned)(L::cb(s) - s) : zaddr;
+    };
+    double ring[4];
+    sfor<0, 4>([&](auto jc) __attribute__((always_inline)) {
+      lds_ld64(ring[decltype(jc)::value], addr(decltype(jc)::value));
+    });
 #pragma unroll 1
-  for (int s = NV - 1; s >= 0; --s) {
-    const int vv = tid < s ? tid : 0;
-    double l = Lc[L::cb(vv) + s - vv];
-    const double zs = Blk<L::W>::bcast(acc, s, red) * invd[s];
-    if (tid == s) z = zs;
-    if (!(tid < s)) l = 0.0;
-    acc = fma(-l, zs, acc);
+    for (int s = 0; s < SEND; s += 4) {
+      sfor<0, 4>([&](auto jc) __attribute__((always_inline)) {
+        constexpr int j = decltype(jc)::value;
+        const int sj = s + j;
+        const double ys = rdlane(acc, sj);
+        if (tid == sj) yp = ys;
+        lds_wait<3>(ring[j]);
+        acc = fma(-ring[j], ys, acc);
+        lds_ld64(ring[j], addr(sj + 4));
+      });
+    }
+    lds_wait<0>(ring[0]);   // drain the ring (its last loads are dummies)
+  } else {
+#pragma unroll 1
+    for (int s = 0; s < NV; ++s) {
+      const double l = *((tid > s && tid < NV) ? Mc + L::cb(s) + (tid - s) : zero);
+      const double ys = Blk<L::W>::bcast(acc, s, red);
+      if (tid == s) yp = ys;
+      acc = fma(-l, ys, acc);
+    }
+  }
+  return yp * dinv;
+}
+// z = L^-T b (lane v holds b_v), M from the LDS copy.  One wave: loads of
+// step s-4 are issued at step s (a 4-deep ring of hand-counted loads).
+template <int N>
+__device__ __forceinline__ double tri_bwd(double acc, const double* Mc, const double* zero,
+                                          double dinv, double* red) {
+  using L = Lay<N>;
+  constexpr int NV = L::NV;
+  constexpr int STOP = ((NV + 3) & ~3) - 1;   // first step, padded (steps >= NV are no-ops)
+  const int tid = threadIdx.x;
+  const int cbt = tid < NV ? L::cb(tid) : 0;
+  acc *= dinv;
+  double z = 0.0;
+  if constexpr (L::W == 1) {
+    // M[s][tid] for tid < s sits at Mc[cbt + s - tid]; other lanes read a 0
+    const unsigned base = lds_addr(Mc + cbt - tid), zaddr = lds_addr(zero);
+    auto addr = [&](int s) -> unsigned {
+      return (tid < s && s < NV && s >= 0) ? base + 8u * (unsigned)s : zaddr;
+    };
+    double ring[4];
+    sfor<0, 4>([&](auto jc) __attribute__((always_inline)) {
+      lds_ld64(ring[decltype(jc)::value], addr(STOP - decltype(jc)::value));
+    });
+#pragma unroll 1
+    for (int s = STOP; s >= 0; s -= 4) {
+      sfor<0, 4>([&](auto jc) __attribute__((always_inline)) {
+        constexpr int j = decltype(jc)::value;
+        const int sj = s - j;
+        const double zs = rdlane(acc, sj);
+        if (tid == sj) z = zs;
+        lds_wait<3>(ring[j]);
+        acc = fma(-ring[j], zs, acc);
+        lds_ld64(ring[j], addr(sj - 4));
+      });
+    }
+    lds_wait<0>(ring[0]);   // drain the ring (its last loads are dummies)
+  } else {
+    auto addr = [&](int s) -> const double* {
+      return (tid < s && s < NV && s >= 0) ? Mc + cbt + (s - tid) : zero;
+    };
+#pragma unroll 1
+    for (int s = STOP; s >= 0; --s) {
+      const double l = *addr(s);
+      const double zs = Blk<L::W>::bcast(acc, s, red);
+      if (tid == s) z = zs;
+      acc = fma(-l, zs, acc);
+    }
   }
   return z;
 }
@@ -493,25 +606,12 @@ solve_kernel(SolveArgs a) {
 
   // ---------------- phase 2: wave-uniform sweeps ----------------------------
   {
-    // free response xbar_{k+1} = Ad_k xbar_k + Gd and gradient terms
-    // d_{k+1} = W_k (xbar_{k+1} - r_k)
+    // one loop runs two independent recursions side by side (ILP):
+    //   free response xbar_{k+1} = Ad_k xbar_k + Gd, d_{k+1} = W_k (xbar_{k+1} - r_k)
+    //   cost-to-go    S_N = W_{N-1} = 100 Q, S_t = Q + Ad_t' S_{t+1} Ad_t, t = N-1-k
     double xb[12];
 #pragma unroll
     for (int r = 0; r < 12; ++r) xb[r] = sm[L::XIN + r];
-    if (tid == 0) sm[L::ZB] = xb[2];
-#pragma unroll 1
-    for (int k = 0; k < N; ++k) {
-      const double cp = sm[L::CS + 2 * k], sp = sm[L::CS + 2 * k + 1];
-      ad_times(xb, dt, cp, sp);
-      xb[8] += -a.g * dt;
-      const double kf = (k == N - 1) ? kTermQ : 1.0;
-      if (tid == 0) {
-        sm[L::ZB + k + 1] = xb[2];
-#pragma unroll
-        for (int r = 0; r < 12; ++r) sm[L::DG + 12 * k + r] = kf * kQ[r] * (xb[r] - sm[L::XREF + 12 * k + r]);
-      }
-    }
-    // S_N = W_{N-1} = 100 Q; S_t = Q + Ad_t' S_{t+1} Ad_t, t = N-1 .. 1
     double s[22];
 #pragma unroll
     for (int a3 = 0; a3 < 3; ++a3) {
@@ -523,47 +623,79 @@ solve_kernel(SolveArgs a) {
     s[12] = kTermQ * kQ[3]; s[13] = 0.0; s[14] = kTermQ * kQ[4];
     s[15] = s[16] = s[17] = s[18] = 0.0;
     s[19] = kTermQ * kQ[9]; s[20] = 0.0; s[21] = kTermQ * kQ[10];
-    if (tid == 0)
+    if (tid == 0) {
+      sm[L::ZB] = xb[2];
 #pragma unroll
       for (int e = 0; e < 22; ++e) sm[L::SS + 22 * (N - 1) + e] = s[e];
+    }
+#pragma unroll 1
+    for (int k = 0; k < N; ++k) {
+      const double cp = sm[L::CS + 2 * k], sp = sm[L::CS + 2 * k + 1];
+      ad_times(xb, dt, cp, sp);
+      xb[8] += -a.g * dt;
+      const double kf = (k == N - 1) ? kTermQ : 1.0;
+      if (tid == 0) {
+        sm[L::ZB + k + 1] = xb[2];
+#pragma unroll
+        for (int r = 0; r < 12; ++r) sm[L::DG + 12 * k + r] = kf * kQ[r] * (xb[r] - sm[L::XREF + 12 * k + r]);
+      }
+      const int t = N - 1 - k;
+      if (t >= 1) {
+        const double ct = sm[L::CS + 2 * t], st = sm[L::CS + 2 * t + 1];
+        // translational axes and yaw: [[a, b], [b, c]] with p' = p + dt v
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int o = 3 * q;
+          const double aa = s[o], bb = s[o + 1], cc = s[o + 2];
+          s[o + 1] = fma(dt, aa, bb);
+          s[o + 2] = cc + dt * (2.0 * bb + dt * aa);
+        }
+        // roll/pitch block, theta' = theta + D w with D = dt [[c, s], [-s, c]]:
+        //   M' = M + P D,   Qm' = Qm + D'(M + P D) + M' D   (old M in the last term)
+        const double D00 = ct * dt, D01 = st * dt, D10 = -st * dt, D11 = ct * dt;
+        const double P00 = s[12], P01 = s[13], P11 = s[14];
+        const double M00 = s[15], M01 = s[16], M10 = s[17], M11 = s[18];
+        const double N00 = M00 + (P00 * D00 + P01 * D10), N01 = M01 + (P00 * D01 + P01 * D11);
+        const double N10 = M10 + (P01 * D00 + P11 * D10), N11 = M11 + (P01 * D01 + P11 * D11);
+        const double A00 = D00 * N00 + D10 * N10, A01 = D00 * N01 + D10 * N11;
+        const double A11 = D01 * N01 + D11 * N11;
+        const double B00 = M00 * D00 + M10 * D10, B01 = M00 * D01 + M10 * D11;
+        const double B11 = M01 * D01 + M11 * D11;
+        s[19] += A00 + B00;
+        s[20] += A01 + B01;
+        s[21] += A11 + B11;
+        s[15] = N00; s[16] = N01; s[17] = N10; s[18] = N11;
+        // + W_{t-1} = Q (diagonal)
+#pragma unroll
+        for (int a3 = 0; a3 < 3; ++a3) {
+          s[3 * a3] += kQ[a3];
+          s[3 * a3 + 2] += kQ[6 + a3];
+        }
+        s[9] += kQ[5]; s[11] += kQ[11];
+        s[12] += kQ[3]; s[14] += kQ[4];
+        s[19] += kQ[9]; s[21] += kQ[10];
+        if (tid == 0)
+#pragma unroll
+          for (int e = 0; e < 22; ++e) sm[L::SS + 22 * (t - 1) + e] = s[e];
+      }
+    }
+    B::sync();
+    // adjoint a_N = d_N, a_t = d_t + Ad_t' a_{t+1}: the gradient of the
+    // tracking cost w.r.t. x_t.  Only rows 6..11 are kept (Bd's nonzero rows).
+    double aj[12];
+#pragma unroll
+    for (int r = 0; r < 12; ++r) aj[r] = sm[L::DG + 12 * (N - 1) + r];
+    if (tid == 0)
+#pragma unroll
+      for (int r = 0; r < 6; ++r) sm[L::AJ + 6 * (N - 1) + r] = aj[6 + r];
 #pragma unroll 1
     for (int t = N - 1; t >= 1; --t) {
-      const double cp = sm[L::CS + 2 * t], sp = sm[L::CS + 2 * t + 1];
-      // translational axes and yaw: [[a, b], [b, c]] with p' = p + dt v
+      adt_times(aj, dt, sm[L::CS + 2 * t], sm[L::CS + 2 * t + 1]);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int o = 3 * q;
-        const double aa = s[o], bb = s[o + 1], cc = s[o + 2];
-        s[o + 1] = fma(dt, aa, bb);
-        s[o + 2] = cc + dt * (2.0 * bb + dt * aa);
-      }
-      // roll/pitch block, theta' = theta + D w with D = dt [[c, s], [-s, c]]:
-      //   M' = M + P D,   Qm' = Qm + D'(M + P D) + M' D   (old M in the last term)
-      const double D00 = cp * dt, D01 = sp * dt, D10 = -sp * dt, D11 = cp * dt;
-      const double P00 = s[12], P01 = s[13], P11 = s[14];
-      const double M00 = s[15], M01 = s[16], M10 = s[17], M11 = s[18];
-      const double N00 = M00 + (P00 * D00 + P01 * D10), N01 = M01 + (P00 * D01 + P01 * D11);
-      const double N10 = M10 + (P01 * D00 + P11 * D10), N11 = M11 + (P01 * D01 + P11 * D11);
-      const double A00 = D00 * N00 + D10 * N10, A01 = D00 * N01 + D10 * N11;
-      const double A11 = D01 * N01 + D11 * N11;
-      const double B00 = M00 * D00 + M10 * D10, B01 = M00 * D01 + M10 * D11;
-      const double B11 = M01 * D01 + M11 * D11;
-      s[19] += A00 + B00;
-      s[20] += A01 + B01;
-      s[21] += A11 + B11;
-      s[15] = N00; s[16] = N01; s[17] = N10; s[18] = N11;
-      // + W_{t-1} = Q (diagonal)
-#pragma unroll
-      for (int a3 = 0; a3 < 3; ++a3) {
-        s[3 * a3] += kQ[a3];
-        s[3 * a3 + 2] += kQ[6 + a3];
-      }
-      s[9] += kQ[5]; s[11] += kQ[11];
-      s[12] += kQ[3]; s[14] += kQ[4];
-      s[19] += kQ[9]; s[21] += kQ[10];
+      for (int r = 0; r < 12; ++r) aj[r] += sm[L::DG + 12 * (t - 1) + r];
       if (tid == 0)
 #pragma unroll
-        for (int e = 0; e < 22; ++e) sm[L::SS + 22 * (t - 1) + e] = s[e];
+        for (int r = 0; r < 6; ++r) sm[L::AJ + 6 * (t - 1) + r] = aj[6 + r];
     }
   }
   __syncthreads();
@@ -601,23 +733,10 @@ solve_kernel(SolveArgs a) {
       hd[c2] = bd_dot<VAR>(c2, f, bwi, dtm, cpi, spi);
       if (c2 == ci && ii != N - 1) hd[c2] += 2.0 * kRdiag;
     }
-    // gradient: h_v = 2 sum_{j >= i} d_{j+1}' e_j, e_j = Phi(j+1, i+1) b
-    double e[12];
-#pragma unroll
-    for (int r = 0; r < 12; ++r) e[r] = 0.0;
+    // gradient: h_v = 2 b' a_{i+1} (b = Bd_i e_c, a = adjoint of phase 2)
     double hacc = 0.0;
-#pragma unroll 1
-    for (int j = 0; j < N; ++j) {
-      const double cp = sm[L::CS + 2 * j], sp = sm[L::CS + 2 * j + 1];
-      ad_times(e, dt, cp, sp);
-      const bool start = (ii == j);
 #pragma unroll
-      for (int r = 0; r < 12; ++r) e[r] = start ? e0[r] : e[r];
-      double dd = 0.0;
-#pragma unroll
-      for (int r = 0; r < 12; ++r) dd = fma(sm[L::DG + 12 * j + r], e[r], dd);
-      if (ii <= j) hacc += dd;
-    }
+    for (int r = 0; r < 6; ++r) hacc = fma(e0[6 + r], sm[L::AJ + 6 * ii + r], hacc);
     // lower part, j < i: H[v, (j, c2)] = 2 Bd_j[:,c2]' g_j,
     // g_i = f, g_j = Ad_{j+1}' g_{j+1}
     double g[12];
@@ -663,70 +782,81 @@ solve_kernel(SolveArgs a) {
   HMPC_STAMP(4);
 
   int status = ST_SOLVED;
+  double dinv = 0.0;
 
   // ---------------- phase 4: Cholesky ---------------------------------------
-  // Register j of the row always holds column j.  Columns go in blocks of 8:
-  // one runtime loop of 8 steps per block, whose body updates registers
-  // [8bb, NV) -- the same code for all 8 steps, so the kernel keeps a small
+  // Register j of the row holds column j.  Columns go in blocks of 8: one
+  // runtime loop of 8 steps per block, whose body updates registers [8bb, NV)
+  // -- the same code for all 8 steps, so the kernel keeps a small
   // instruction footprint.  Step k publishes column k (lanes >= k) through
-  // LDS; registers of already-eliminated columns take harmless garbage.
+  // LDS.  Register k then takes M[tid][k] = L[tid][k] / L[k][k] (1/L[k][k] on
+  // the diagonal, 0 above it): after the last step the row IS row tid of M,
+  // which the forward sweeps read straight from registers.  The column-major
+  // copy in LDS serves the backward sweeps.  The next step's column value is
+  // picked out of the registers while this step's FMAs stream, and the column
+  // loads go out before the pivot arithmetic (hand-counted waits).
   {
     double* Lc = sm + L::LC;
-    double* invd = sm + L::INVD;
+    if (tid == 0) sm[L::ZR] = 0.0;
+    double mine = Rg[0];   // A[tid][k] of the current step
+    dinv = 0.0;            // 1 / L[tid][tid]
     sfor<0, (NV + 7) / 8>([&](auto bc) __attribute__((always_inline)) {
       constexpr int bb = decltype(bc)::value;
       constexpr int J0 = 8 * bb;
       constexpr int KEND = (J0 + 8 < NV) ? J0 + 8 : NV;
       constexpr int NCH = (NV - J0 + 7) / 8;   // chunks of 8 registers in [J0, NV)
+      // b128 loads of chunk ch (the last chunk may be short)
+      auto nld = [](int ch) constexpr { return (NV - J0 - 8 * ch) >= 8 ? 4 : (NV - J0 - 8 * ch + 1) / 2; };
 #pragma unroll 1
       for (int k = J0; k < KEND; ++k) {
-        const int kk = k - J0;
         double* col = sm + L::COLB + (k & 1) * (NT + 8);
-        // mine = Rg[k] = A[tid][k] (current).  The pins hide the select chain
-        // from the pattern that would turn it into a dynamic index (and the
-        // whole row into scratch).
-        double mine = Rg[J0];
-        pin(mine);
-        sfor<1, KEND - J0>([&](auto jc) __attribute__((always_inline)) {
-          constexpr int jj = decltype(jc)::value;
-          double c = Rg[J0 + jj];
-          pin(c);
-          mine = (kk == jj) ? c : mine;
-        });
         col[tid] = (tid >= k && tid < NV) ? mine : 0.0;
         B::sync();
-        const double piv = (W == 1) ? rdlane(mine, k) : col[k];
-        const double pv = piv > 0.0 ? piv : 1.0;
-        if (!(piv > 0.0)) status = ST_NUMERICAL;
-        const double rs = 1.0 / sqrt(pv);
-        const double lik = mine * rs;
-        if (tid >= k && tid < NV) Lc[L::cb(k) + tid - k] = lik;
-        if (tid == k) invd[k] = rs;
-        const double nt = (tid > k && tid < NV) ? -lik * rs : 0.0;
-        // Rg[j] += nt * col[j], j in [J0, NV): 16-byte loads, one chunk ahead
-        const double2* c2 = reinterpret_cast<const double2*>(col + J0);
-        double2 buf[2][4];
+        double piv = 0.0;
+        if constexpr (W > 1) piv = col[k];
+        const unsigned cbase = lds_addr(col + J0);
+        dbl2 buf[3][4];
         auto load = [&](auto chc) __attribute__((always_inline)) {
           constexpr int ch = decltype(chc)::value;
-          const double2* pp = c2 + 4 * ch + opaque_zero();
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-            if (J0 + 8 * ch + 2 * i < NV) buf[ch & 1][i] = pp[i];
+          if constexpr (ch < NCH) {
+            sfor<0, nld(ch)>([&](auto ic) __attribute__((always_inline)) {
+              constexpr int i = decltype(ic)::value;
+              lds_ld128<64 * ch + 16 * i>(buf[ch % 3][i], cbase);
+            });
+          }
         };
         load(std::integral_constant<int, 0>{});
+        load(std::integral_constant<int, 1>{});
+        if constexpr (W == 1) piv = rdlane(mine, k);
+        const double pv = piv > 0.0 ? piv : 1.0;
+        if (!(piv > 0.0)) status = ST_NUMERICAL;
+        const double rs = rsq_nr(pv);
+        const double tk = (mine * rs) * rs;   // M[tid][k] = L[tid][k] / L[k][k]
+        const double mk = (tid > k && tid < NV) ? tk : ((tid == k) ? rs : 0.0);
+        const double nt = (tid > k && tid < NV) ? -tk : 0.0;
+        dinv = (tid == k) ? rs : dinv;
+        double nxt = 0.0;
         sfor<0, NCH>([&](auto chc) __attribute__((always_inline)) {
           constexpr int ch = decltype(chc)::value;
-          if constexpr (ch + 1 < NCH) load(std::integral_constant<int, ch + 1>{});
+          load(std::integral_constant<int, ch + 2>{});
+          // LDS instructions issued after chunk ch's loads
+          constexpr int younger = (ch + 1 < NCH ? nld(ch + 1) : 0) + (ch + 2 < NCH ? nld(ch + 2) : 0);
+          lds_wait<younger>(buf[ch % 3][0], buf[ch % 3][1], buf[ch % 3][2], buf[ch % 3][3]);
           sfor<0, 8>([&](auto ic) __attribute__((always_inline)) {
             constexpr int i = decltype(ic)::value;
             constexpr int j = J0 + 8 * ch + i;
             if constexpr (j < NV) {
-              const double cv = (i & 1) ? buf[ch & 1][i / 2].y : buf[ch & 1][i / 2].x;
-              Rg[j] = fma(nt, cv, Rg[j]);
+              const double cv = (i & 1) ? buf[ch % 3][i / 2].y : buf[ch % 3][i / 2].x;
+              double r = fma(nt, cv, Rg[j]);
+              if constexpr (j < KEND) r = (j == k) ? mk : r;
+              Rg[j] = r;
               pin(Rg[j]);
+              if constexpr (j > J0 && j <= J0 + 8) nxt = (j == k + 1) ? Rg[j] : nxt;
             }
           });
         });
+        if (tid >= k && tid < NV) Lc[L::cb(k) + tid - k] = mk;
+        mine = nxt;
       }
     });
     __syncthreads();
@@ -734,13 +864,13 @@ solve_kernel(SolveArgs a) {
   HMPC_STAMP(5);
 
   const double* Lc = sm + L::LC;
-  const double* invd = sm + L::INVD;
+  const double* zero = sm + L::ZR;
 
   // ---------------- phase 5: v0 = -L^-T L^-1 h -------------------------------
   double v = 0.0;
   {
-    const double y = tri_fwd<N>(-hv, 0, Lc, invd, red);
-    v = tri_bwd<N>(y, Lc, invd, red);
+    const double y = tri_fwd<N>(-hv, Rg, dinv, red);
+    v = tri_bwd<N>(y, Lc, zero, dinv, red);
   }
   HMPC_STAMP(6);
 
@@ -859,9 +989,8 @@ solve_kernel(SolveArgs a) {
     const double bp = rhs_of(p);
     const double np_me = coef_of(p, tid);
     double u_plus = 0.0;
-    // w = L^-1 n_p, from the first nonzero of n_p on
-    const int s0 = B::first(np_me != 0.0, red);
-    const double wfull = tri_fwd<N>(np_me, s0 < 0 ? NV : s0, Lc, invd, red);
+    // w = L^-1 n_p
+    const double wfull = tri_fwd_lds<N>(np_me, Lc, zero, dinv, red);
     const double wnorm2 = B::sum(wfull * wfull, red);
 
     // ---- inner loop: step towards satisfying constraint p ----
@@ -886,7 +1015,7 @@ solve_kernel(SolveArgs a) {
       }
       B::sync();
       // primal direction z = L^-T w_perp (lane v gets z_v)
-      const double zi = tri_bwd<N>(wp, Lc, invd, red);
+      const double zi = tri_bwd<N>(wp, Lc, zero, dinv, red);
       // dual direction r = R^-1 c (lanes l < q), back substitution
       double rcur = tid < qu ? cbv[tid] : 0.0, rmine = 0.0;
       for (int l = qu - 1; l >= 0; --l) {
