@@ -365,22 +365,20 @@ __device__ __forceinline__ double bd_dot(int c2, const double (&y)[12], const do
 // step's dependent chain is just readlane -> fma.
 // ----------------------------------------------------------------------------
 // y = L^-1 b (lane v holds b_v), M from registers, fully unrolled.
-// Mr[s] = M[tid][s] below the diagonal, 1/L_ss on it (the stale update of
-// the finished lane is harmless) and 0 above.
+// Mr[s] = M[tid][s] below the diagonal and 0 on and above it.
 template <int N>
 __device__ __forceinline__ double tri_fwd(double acc, const double (&Mr)[6 * N], double dinv,
                                           double* red) {
   using L = Lay<N>;
   constexpr int NV = L::NV;
   const int tid = threadIdx.x;
-  double yp = 0.0;
+  (void)tid;
   sfor<0, NV>([&](auto sc) __attribute__((always_inline)) {
     constexpr int s = decltype(sc)::value;
-    const double ys = Blk<L::W>::bcast(acc, s, red);
-    if (tid == s) yp = ys;
-    acc = fma(-Mr[s], ys, acc);
+    acc = fma(-Mr[s], Blk<L::W>::bcast(acc, s, red), acc);
   });
-  return yp * dinv;
+  // lane v's accumulator is final once step v has read it (M[v][s] = 0, s >= v)
+  return acc * dinv;
 }
 // The same sweep from the LDS copy (the active-set phase, where the
 // registers hold the Gram-Schmidt basis instead): loads of step s+4 are
@@ -392,7 +390,6 @@ __device__ __forceinline__ double tri_fwd_lds(double acc, const double* Mc, cons
   constexpr int NV = L::NV;
   constexpr int SEND = (NV + 3) & ~3;   // padded (steps >= NV are no-ops)
   const int tid = threadIdx.x;
-  double yp = 0.0;
   if constexpr (L::W == 1) {
     // M[tid][s] for tid > s sits at Mc[cb(s) + tid - s]; other lanes read a 0
     const unsigned base = lds_addr(Mc + tid), zaddr = lds_addr(zero);
@@ -409,7 +406,6 @@ __device__ __forceinline__ double tri_fwd_lds(double acc, const double* Mc, cons
         constexpr int j = decltype(jc)::value;
         const int sj = s + j;
         const double ys = rdlane(acc, sj);
-        if (tid == sj) yp = ys;
         lds_wait<3>(ring[j]);
         acc = fma(-ring[j], ys, acc);
         lds_ld64(ring[j], addr(sj + 4));
@@ -420,12 +416,11 @@ __device__ __forceinline__ double tri_fwd_lds(double acc, const double* Mc, cons
 #pragma unroll 1
     for (int s = 0; s < NV; ++s) {
       const double l = *((tid > s && tid < NV) ? Mc + L::cb(s) + (tid - s) : zero);
-      const double ys = Blk<L::W>::bcast(acc, s, red);
-      if (tid == s) yp = ys;
-      acc = fma(-l, ys, acc);
+      acc = fma(-l, Blk<L::W>::bcast(acc, s, red), acc);
     }
   }
-  return yp * dinv;
+  // lane v's accumulator is final once step v has read it
+  return acc * dinv;
 }
 // z = L^-T b (lane v holds b_v), M from the LDS copy.  One wave: loads of
 // step s-4 are issued at step s (a 4-deep ring of hand-counted loads).
@@ -438,7 +433,6 @@ __device__ __forceinline__ double tri_bwd(double acc, const double* Mc, const do
   const int tid = threadIdx.x;
   const int cbt = tid < NV ? L::cb(tid) : 0;
   acc *= dinv;
-  double z = 0.0;
   if constexpr (L::W == 1) {
     // M[s][tid] for tid < s sits at Mc[cbt + s - tid]; other lanes read a 0
     const unsigned base = lds_addr(Mc + cbt - tid), zaddr = lds_addr(zero);
@@ -455,7 +449,6 @@ __device__ __forceinline__ double tri_bwd(double acc, const double* Mc, const do
         constexpr int j = decltype(jc)::value;
         const int sj = s - j;
         const double zs = rdlane(acc, sj);
-        if (tid == sj) z = zs;
         lds_wait<3>(ring[j]);
         acc = fma(-ring[j], zs, acc);
         lds_ld64(ring[j], addr(sj - 4));
@@ -469,12 +462,10 @@ __device__ __forceinline__ double tri_bwd(double acc, const double* Mc, const do
 #pragma unroll 1
     for (int s = STOP; s >= 0; --s) {
       const double l = *addr(s);
-      const double zs = Blk<L::W>::bcast(acc, s, red);
-      if (tid == s) z = zs;
-      acc = fma(-l, zs, acc);
+      acc = fma(-l, Blk<L::W>::bcast(acc, s, red), acc);
     }
   }
-  return z;
+  return acc;   // lane v's accumulator is final once step v has read it
 }
 
 // ----------------------------------------------------------------------------
@@ -785,81 +776,139 @@ solve_kernel(SolveArgs a) {
   double dinv = 0.0;
 
   // ---------------- phase 4: Cholesky ---------------------------------------
-  // Register j of the row holds column j.  Columns go in blocks of 8: one
-  // runtime loop of 8 steps per block, whose body updates registers [8bb, NV)
-  // -- the same code for all 8 steps, so the kernel keeps a small
-  // instruction footprint.  Step k publishes column k (lanes >= k) through
-  // LDS.  Register k then takes M[tid][k] = L[tid][k] / L[k][k] (1/L[k][k] on
-  // the diagonal, 0 above it): after the last step the row IS row tid of M,
-  // which the forward sweeps read straight from registers.  The column-major
-  // copy in LDS serves the backward sweeps.  The next step's column value is
-  // picked out of the registers while this step's FMAs stream, and the column
-  // loads go out before the pivot arithmetic (hand-counted waits).
+  // Right-looking, lane v holds row v of the trailing matrix in registers
+  // (register j = column j).  Step k publishes column k (lanes >= k) through
+  // LDS; every lane then updates its registers j > k.  Afterwards register k
+  // holds M[tid][k] = L[tid][k] / L[k][k] below the diagonal (0 elsewhere):
+  // the row IS row tid of M, which the forward sweep reads from registers.
+  // A column-major copy of M (1/L_kk on the diagonal) goes to LDS for the
+  // backward sweeps.  Column loads are issued before the pivot arithmetic
+  // (hand-counted waits).
+  //   NV <= 64 (one wave): every step unrolled -- no runtime index, no selects.
+  //   NV >  64: blocks of 8 steps share one runtime loop body (code size).
   {
-    double* Lc = sm + L::LC;
     if (tid == 0) sm[L::ZR] = 0.0;
-    double mine = Rg[0];   // A[tid][k] of the current step
-    dinv = 0.0;            // 1 / L[tid][tid]
-    sfor<0, (NV + 7) / 8>([&](auto bc) __attribute__((always_inline)) {
-      constexpr int bb = decltype(bc)::value;
-      constexpr int J0 = 8 * bb;
-      constexpr int KEND = (J0 + 8 < NV) ? J0 + 8 : NV;
-      constexpr int NCH = (NV - J0 + 7) / 8;   // chunks of 8 registers in [J0, NV)
-      // b128 loads of chunk ch (the last chunk may be short)
-      auto nld = [](int ch) constexpr { return (NV - J0 - 8 * ch) >= 8 ? 4 : (NV - J0 - 8 * ch + 1) / 2; };
-#pragma unroll 1
-      for (int k = J0; k < KEND; ++k) {
+    // non-positive pivots, counted: `if (piv <= 0) status = ...` per step
+    // kept 60 condition masks alive in SGPRs (and spilled)
+    double nbad = 0.0;
+    auto nld_of = [](int lo, int ch) constexpr {   // b128 loads of chunk ch of [lo, NV)
+      return (NV - lo - 8 * ch) >= 8 ? 4 : (NV - lo - 8 * ch + 1) / 2;
+    };
+    if constexpr (W == 1) {
+      sfor<0, NV>([&](auto kc) __attribute__((always_inline)) {
+        constexpr int k = decltype(kc)::value;
+        constexpr int JA = (k + 1) & ~1;            // 16-B aligned start of the update
+        constexpr int NCH = (NV - JA + 7) / 8;      // chunks of 8 columns
+        // lane masks and addresses of this step are computed from an opaque
+        // copy of k: hoisted out of the unrolled steps they would pin ~100
+        // SGPRs for the whole factorisation (and spill)
+        const int ko = k + opaque_zero();
         double* col = sm + L::COLB + (k & 1) * (NT + 8);
-        col[tid] = (tid >= k && tid < NV) ? mine : 0.0;
+        const double mine = Rg[k];
+        col[tid] = (tid >= ko && tid < NV) ? mine : 0.0;
         B::sync();
-        double piv = 0.0;
-        if constexpr (W > 1) piv = col[k];
-        const unsigned cbase = lds_addr(col + J0);
-        dbl2 buf[3][4];
+        const unsigned cbase = lds_addr(col + JA);
+        dbl2 buf[2][4];
         auto load = [&](auto chc) __attribute__((always_inline)) {
           constexpr int ch = decltype(chc)::value;
           if constexpr (ch < NCH) {
-            sfor<0, nld(ch)>([&](auto ic) __attribute__((always_inline)) {
+            sfor<0, nld_of(JA, ch)>([&](auto ic) __attribute__((always_inline)) {
               constexpr int i = decltype(ic)::value;
-              lds_ld128<64 * ch + 16 * i>(buf[ch % 3][i], cbase);
+              lds_ld128<64 * ch + 16 * i>(buf[ch % 2][i], cbase);
             });
           }
         };
         load(std::integral_constant<int, 0>{});
-        load(std::integral_constant<int, 1>{});
-        if constexpr (W == 1) piv = rdlane(mine, k);
+        const double piv = rdlane(mine, k);
         const double pv = piv > 0.0 ? piv : 1.0;
-        if (!(piv > 0.0)) status = ST_NUMERICAL;
+        nbad += (piv > 0.0) ? 0.0 : 1.0;   // folded into status after the loop
+        pin(nbad);                          // (materialised here, not sunk to the end)
         const double rs = rsq_nr(pv);
-        const double tk = (mine * rs) * rs;   // M[tid][k] = L[tid][k] / L[k][k]
-        const double mk = (tid > k && tid < NV) ? tk : ((tid == k) ? rs : 0.0);
-        const double nt = (tid > k && tid < NV) ? -tk : 0.0;
-        dinv = (tid == k) ? rs : dinv;
-        double nxt = 0.0;
+        const double tk = (mine * rs) * rs;   // M[tid][k]
+        const bool below = tid > ko && tid < NV;
+        const double nt = below ? -tk : 0.0;
         sfor<0, NCH>([&](auto chc) __attribute__((always_inline)) {
           constexpr int ch = decltype(chc)::value;
-          load(std::integral_constant<int, ch + 2>{});
-          // LDS instructions issued after chunk ch's loads
-          constexpr int younger = (ch + 1 < NCH ? nld(ch + 1) : 0) + (ch + 2 < NCH ? nld(ch + 2) : 0);
-          lds_wait<younger>(buf[ch % 3][0], buf[ch % 3][1], buf[ch % 3][2], buf[ch % 3][3]);
+          load(std::integral_constant<int, ch + 1>{});
+          constexpr int younger = ch + 1 < NCH ? nld_of(JA, ch + 1) : 0;
+          lds_wait<younger>(buf[ch % 2][0], buf[ch % 2][1], buf[ch % 2][2], buf[ch % 2][3]);
           sfor<0, 8>([&](auto ic) __attribute__((always_inline)) {
             constexpr int i = decltype(ic)::value;
-            constexpr int j = J0 + 8 * ch + i;
-            if constexpr (j < NV) {
-              const double cv = (i & 1) ? buf[ch % 3][i / 2].y : buf[ch % 3][i / 2].x;
-              double r = fma(nt, cv, Rg[j]);
-              if constexpr (j < KEND) r = (j == k) ? mk : r;
-              Rg[j] = r;
+            constexpr int j = JA + 8 * ch + i;
+            if constexpr (j > k && j < NV) {
+              const double cv = (i & 1) ? buf[ch % 2][i / 2].y : buf[ch % 2][i / 2].x;
+              Rg[j] = fma(nt, cv, Rg[j]);
               pin(Rg[j]);
-              if constexpr (j > J0 && j <= J0 + 8) nxt = (j == k + 1) ? Rg[j] : nxt;
             }
           });
         });
-        if (tid >= k && tid < NV) Lc[L::cb(k) + tid - k] = mk;
-        mine = nxt;
-      }
-    });
+        Rg[k] = below ? tk : 0.0;
+        // branch-free store of column k of M (other lanes: the idle buffer)
+        const int o_l = L::LC + L::cb(k) + (tid - ko);
+        const int o_d = L::COLB + ((k + 1) & 1) * (NT + 8) + tid;
+        sm[(tid >= ko && tid < NV) ? o_l : o_d] = (tid == ko) ? rs : tk;
+      });
+    } else {
+      double mine = Rg[0];   // A[tid][k] of the current step
+      sfor<0, (NV + 7) / 8>([&](auto bc) __attribute__((always_inline)) {
+        constexpr int bb = decltype(bc)::value;
+        constexpr int J0 = 8 * bb;
+        constexpr int KEND = (J0 + 8 < NV) ? J0 + 8 : NV;
+        constexpr int NCH = (NV - J0 + 7) / 8;
+#pragma unroll 1
+        for (int k = J0; k < KEND; ++k) {
+          double* col = sm + L::COLB + (k & 1) * (NT + 8);
+          col[tid] = (tid >= k && tid < NV) ? mine : 0.0;
+          B::sync();
+          const double piv = col[k];
+          const unsigned cbase = lds_addr(col + J0);
+          dbl2 buf[2][4];
+          auto load = [&](auto chc) __attribute__((always_inline)) {
+            constexpr int ch = decltype(chc)::value;
+            if constexpr (ch < NCH) {
+              sfor<0, nld_of(J0, ch)>([&](auto ic) __attribute__((always_inline)) {
+                constexpr int i = decltype(ic)::value;
+                lds_ld128<64 * ch + 16 * i>(buf[ch % 2][i], cbase);
+              });
+            }
+          };
+          load(std::integral_constant<int, 0>{});
+          const double pv = piv > 0.0 ? piv : 1.0;
+          nbad += (piv > 0.0) ? 0.0 : 1.0;   // folded into status after the loop
+        pin(nbad);                          // (materialised here, not sunk to the end)
+          const double rs = rsq_nr(pv);
+          const double tk = (mine * rs) * rs;
+          const bool below = tid > k && tid < NV;
+          const double mk = below ? tk : 0.0;
+          const double nt = below ? -tk : 0.0;
+          double nxt = 0.0;
+          sfor<0, NCH>([&](auto chc) __attribute__((always_inline)) {
+            constexpr int ch = decltype(chc)::value;
+            load(std::integral_constant<int, ch + 1>{});
+            constexpr int younger = ch + 1 < NCH ? nld_of(J0, ch + 1) : 0;
+            lds_wait<younger>(buf[ch % 2][0], buf[ch % 2][1], buf[ch % 2][2], buf[ch % 2][3]);
+            sfor<0, 8>([&](auto ic) __attribute__((always_inline)) {
+              constexpr int i = decltype(ic)::value;
+              constexpr int j = J0 + 8 * ch + i;
+              if constexpr (j < NV) {
+                const double cv = (i & 1) ? buf[ch % 2][i / 2].y : buf[ch % 2][i / 2].x;
+                double r = fma(nt, cv, Rg[j]);
+                if constexpr (j < KEND) r = (j == k) ? mk : r;
+                Rg[j] = r;
+                pin(Rg[j]);
+                if constexpr (j > J0 && j <= J0 + 8) nxt = (j == k + 1) ? Rg[j] : nxt;
+              }
+            });
+          });
+          if (tid >= k && tid < NV) sm[L::LC + L::cb(k) + tid - k] = (tid == k) ? rs : tk;
+          mine = nxt;
+          __syncthreads();   // every wave is done with col before step k+2 rewrites it
+        }
+      });
+    }
     __syncthreads();
+    if (nbad != 0.0) status = ST_NUMERICAL;
+    dinv = tid < NV ? sm[L::LC + L::cb(tid < NV ? tid : 0)] : 0.0;   // 1 / L[tid][tid]
   }
   HMPC_STAMP(5);
 
