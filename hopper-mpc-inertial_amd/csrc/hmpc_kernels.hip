@@ -123,6 +123,10 @@ __device__ __forceinline__ void lds_wait(dbl2& a, dbl2& b, dbl2& c, dbl2& d) {
   asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(a), "+v"(b), "+v"(c), "+v"(d) : "i"(CNT));
 }
 template <int CNT>
+__device__ __forceinline__ void lds_wait(dbl2& a, dbl2& b) {
+  asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(a), "+v"(b) : "i"(CNT));
+}
+template <int CNT>
 __device__ __forceinline__ void lds_wait(double& a) {
   asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(a) : "i"(CNT));
 }
@@ -330,6 +334,35 @@ __device__ __forceinline__ void adt_times(double (&g)[12], double dt, double cp,
   g[11] = fma(dt, g[5], g[11]);
 }
 
+// The same two maps lane-parallel: lane r < 12 holds component r.  The
+// cross terms come from other lanes (readlane / bpermute); lanes >= 12 pass
+// their value through unchanged.
+__device__ __forceinline__ double ad_lane(double x, double dt, double cp, double sp) {
+  const int r = threadIdx.x;
+  const double xv = __shfl(x, (int)((threadIdx.x + 6) & 63), 64);   // x[r+6] for r < 3
+  const double w0 = rdlane(x, 9), w1 = rdlane(x, 10), w2 = rdlane(x, 11);
+  double d = 0.0;
+  d = (r < 3) ? xv : d;
+  d = (r == 3) ? (cp * w0 + sp * w1) : d;
+  d = (r == 4) ? (cp * w1 - sp * w0) : d;
+  d = (r == 5) ? w2 : d;
+  return fma(dt, d, x);
+}
+__device__ __forceinline__ double adt_lane(double g, double dt, double cp, double sp) {
+  const int r = threadIdx.x;
+  const double gv = __shfl(g, (int)((threadIdx.x + 58) & 63), 64);  // g[r-6] for 6 <= r < 9
+  const double g3 = rdlane(g, 3), g4 = rdlane(g, 4), g5 = rdlane(g, 5);
+  double d = 0.0;
+  d = (r >= 6 && r < 9) ? gv : d;
+  d = (r == 9) ? (cp * g3 - sp * g4) : d;
+  d = (r == 10) ? (sp * g3 + cp * g4) : d;
+  d = (r == 11) ? g5 : d;
+  return fma(dt, d, g);
+}
+__device__ __forceinline__ double qdiag(int r) {   // Q[r][r], 0 beyond the state
+  return (r == 0 || r == 1 || r == 5) ? 50.0 : (r == 2 ? 2.0 : (r >= 9 && r < 12) ? 10.0 : (r < 12 ? 1.0 : 0.0));
+}
+
 // rows 6..8 of Bd_k, column c2 (< 3): 3f dt/m I (:28), 2f Rz'(psi) dt/m (2f :87)
 template <int VAR>
 __device__ __forceinline__ double bv(int r, int c2, double dtm, double cp, double sp) {
@@ -482,6 +515,9 @@ __device__ __forceinline__ double tri_bwd(double acc, const double* Mc, const do
 #define HMPC_STAMP(i) ((void)0)
 #endif
 
+#ifndef HMPC_CW
+#define HMPC_CW 4
+#endif
 #ifndef HMPC_WAVES_PER_EU
 #define HMPC_WAVES_PER_EU(W) ((W) == 1 ? 2 : 1)
 #endif
@@ -598,11 +634,11 @@ solve_kernel(SolveArgs a) {
   // ---------------- phase 2: wave-uniform sweeps ----------------------------
   {
     // one loop runs two independent recursions side by side (ILP):
-    //   free response xbar_{k+1} = Ad_k xbar_k + Gd, d_{k+1} = W_k (xbar_{k+1} - r_k)
-    //   cost-to-go    S_N = W_{N-1} = 100 Q, S_t = Q + Ad_t' S_{t+1} Ad_t, t = N-1-k
-    double xb[12];
-#pragma unroll
-    for (int r = 0; r < 12; ++r) xb[r] = sm[L::XIN + r];
+    //   free response (lane r < 12 holds xbar[r]) xbar_{k+1} = Ad_k xbar_k + Gd,
+    //     d_{k+1} = W_k (xbar_{k+1} - r_k)
+    //   cost-to-go (wave-uniform) S_N = W_{N-1} = 100 Q, S_t = Q + Ad_t' S_{t+1} Ad_t
+    double xr = tid < 12 ? sm[L::XIN + tid] : 0.0;
+    const double qr = qdiag(tid);
     double s[22];
 #pragma unroll
     for (int a3 = 0; a3 < 3; ++a3) {
@@ -614,22 +650,18 @@ solve_kernel(SolveArgs a) {
     s[12] = kTermQ * kQ[3]; s[13] = 0.0; s[14] = kTermQ * kQ[4];
     s[15] = s[16] = s[17] = s[18] = 0.0;
     s[19] = kTermQ * kQ[9]; s[20] = 0.0; s[21] = kTermQ * kQ[10];
+    if (tid == 2) sm[L::ZB] = xr;
     if (tid == 0) {
-      sm[L::ZB] = xb[2];
 #pragma unroll
       for (int e = 0; e < 22; ++e) sm[L::SS + 22 * (N - 1) + e] = s[e];
     }
 #pragma unroll 1
     for (int k = 0; k < N; ++k) {
       const double cp = sm[L::CS + 2 * k], sp = sm[L::CS + 2 * k + 1];
-      ad_times(xb, dt, cp, sp);
-      xb[8] += -a.g * dt;
+      xr = ad_lane(xr, dt, cp, sp) + ((tid == 8) ? -a.g * dt : 0.0);
       const double kf = (k == N - 1) ? kTermQ : 1.0;
-      if (tid == 0) {
-        sm[L::ZB + k + 1] = xb[2];
-#pragma unroll
-        for (int r = 0; r < 12; ++r) sm[L::DG + 12 * k + r] = kf * kQ[r] * (xb[r] - sm[L::XREF + 12 * k + r]);
-      }
+      if (tid < 12) sm[L::DG + 12 * k + tid] = kf * qr * (xr - sm[L::XREF + 12 * k + tid]);
+      if (tid == 2) sm[L::ZB + k + 1] = xr;
       const int t = N - 1 - k;
       if (t >= 1) {
         const double ct = sm[L::CS + 2 * t], st = sm[L::CS + 2 * t + 1];
@@ -671,41 +703,35 @@ solve_kernel(SolveArgs a) {
       }
     }
     B::sync();
-    // adjoint a_N = d_N, a_t = d_t + Ad_t' a_{t+1}: the gradient of the
-    // tracking cost w.r.t. x_t.  Only rows 6..11 are kept (Bd's nonzero rows).
-    double aj[12];
-#pragma unroll
-    for (int r = 0; r < 12; ++r) aj[r] = sm[L::DG + 12 * (N - 1) + r];
-    if (tid == 0)
-#pragma unroll
-      for (int r = 0; r < 6; ++r) sm[L::AJ + 6 * (N - 1) + r] = aj[6 + r];
+    // adjoint a_N = d_N, a_t = d_t + Ad_t' a_{t+1} (lane-parallel): the
+    // gradient of the tracking cost w.r.t. x_t.  Only rows 6..11 are kept
+    // (the nonzero rows of Bd).
+    double ar = tid < 12 ? sm[L::DG + 12 * (N - 1) + tid] : 0.0;
+    if (tid >= 6 && tid < 12) sm[L::AJ + 6 * (N - 1) + tid - 6] = ar;
 #pragma unroll 1
     for (int t = N - 1; t >= 1; --t) {
-      adt_times(aj, dt, sm[L::CS + 2 * t], sm[L::CS + 2 * t + 1]);
-#pragma unroll
-      for (int r = 0; r < 12; ++r) aj[r] += sm[L::DG + 12 * (t - 1) + r];
-      if (tid == 0)
-#pragma unroll
-        for (int r = 0; r < 6; ++r) sm[L::AJ + 6 * (t - 1) + r] = aj[6 + r];
+      ar = adt_lane(ar, dt, sm[L::CS + 2 * t], sm[L::CS + 2 * t + 1]) +
+           (tid < 12 ? sm[L::DG + 12 * (t - 1) + tid] : 0.0);
+      if (tid >= 6 && tid < 12) sm[L::AJ + 6 * (t - 1) + tid - 6] = ar;
     }
   }
   __syncthreads();
   HMPC_STAMP(3);
 
   // ---------------- phase 3: Hessian row (lower part) + gradient ------------
-  const int vj = tid / 6, vc = tid - 6 * (tid / 6);   // stage / component of my variable
+  const int vj3 = tid / 6, vc3 = tid - 6 * (tid / 6);   // stage / component of my variable
   const bool active_lane = tid < NV;
   const double ubar_z_alias = (sm[L::CC + N - 1] != 0.0) ? 2.0 * a.m * a.g : 0.0;
   auto is_fixed = [&](int k, int c) -> bool {   // swing f = 0 (:134-136), 2f fy = 0 (2f :129)
     return (c < 3 && sm[L::CC + k] == 0.0) || (VAR == 2 && c == 1);
   };
-  const bool my_fixed = active_lane && is_fixed(vj, vc);
+  const bool my_fixed = active_lane && is_fixed(vj3, vc3);
 
   double Rg[NV];   // row `tid` of H (lower part), then the Cholesky trailing row
   double hv = 0.0;
   {
-    const int ii = active_lane ? vj : 0;
-    const int ci = active_lane ? vc : 0;
+    const int ii = active_lane ? vj3 : 0;
+    const int ci = active_lane ? vc3 : 0;
     // my impulse b = Bd_i e_c (rows 6..11) and f = S_{i+1} b
     const double cpi = sm[L::CS + 2 * ii], spi = sm[L::CS + 2 * ii + 1];
     const double* bwi = sm + L::BW + 18 * ii;
@@ -764,8 +790,8 @@ solve_kernel(SolveArgs a) {
     });
     if (active_lane && !my_fixed) {
       double ub = 0.0;
-      if (vc == 2) ub = a.uref_aliased ? ubar_z_alias : ((sm[L::CC + vj] != 0.0) ? 2.0 * a.m * a.g : 0.0);
-      const double Vj = (vj == N - 1) ? 0.0 : kRdiag;
+      if (vc3 == 2) ub = a.uref_aliased ? ubar_z_alias : ((sm[L::CC + vj3] != 0.0) ? 2.0 * a.m * a.g : 0.0);
+      const double Vj = (vj3 == N - 1) ? 0.0 : kRdiag;
       hv = 2.0 * hacc - 2.0 * Vj * ub;
     }
   }
@@ -798,7 +824,8 @@ solve_kernel(SolveArgs a) {
       sfor<0, NV>([&](auto kc) __attribute__((always_inline)) {
         constexpr int k = decltype(kc)::value;
         constexpr int JA = (k + 1) & ~1;            // 16-B aligned start of the update
-        constexpr int NCH = (NV - JA + 7) / 8;      // chunks of 8 columns
+        constexpr int CW = HMPC_CW;                 // columns per load chunk (4 or 8)
+        constexpr int NCH = (NV - JA + CW - 1) / CW;
         // lane masks and addresses of this step are computed from an opaque
         // copy of k: hoisted out of the unrolled steps they would pin ~100
         // SGPRs for the whole factorisation (and spill)
@@ -808,13 +835,16 @@ solve_kernel(SolveArgs a) {
         col[tid] = (tid >= ko && tid < NV) ? mine : 0.0;
         B::sync();
         const unsigned cbase = lds_addr(col + JA);
-        dbl2 buf[2][4];
+        auto nldc = [](int ch) constexpr {   // b128 loads of chunk ch of [JA, NV)
+          return (NV - JA - CW * ch) >= CW ? CW / 2 : (NV - JA - CW * ch + 1) / 2;
+        };
+        dbl2 buf[2][CW / 2];
         auto load = [&](auto chc) __attribute__((always_inline)) {
           constexpr int ch = decltype(chc)::value;
           if constexpr (ch < NCH) {
-            sfor<0, nld_of(JA, ch)>([&](auto ic) __attribute__((always_inline)) {
+            sfor<0, nldc(ch)>([&](auto ic) __attribute__((always_inline)) {
               constexpr int i = decltype(ic)::value;
-              lds_ld128<64 * ch + 16 * i>(buf[ch % 2][i], cbase);
+              lds_ld128<8 * CW * ch + 16 * i>(buf[ch % 2][i], cbase);
             });
           }
         };
@@ -830,11 +860,14 @@ solve_kernel(SolveArgs a) {
         sfor<0, NCH>([&](auto chc) __attribute__((always_inline)) {
           constexpr int ch = decltype(chc)::value;
           load(std::integral_constant<int, ch + 1>{});
-          constexpr int younger = ch + 1 < NCH ? nld_of(JA, ch + 1) : 0;
-          lds_wait<younger>(buf[ch % 2][0], buf[ch % 2][1], buf[ch % 2][2], buf[ch % 2][3]);
-          sfor<0, 8>([&](auto ic) __attribute__((always_inline)) {
+          constexpr int younger = ch + 1 < NCH ? nldc(ch + 1) : 0;
+          if constexpr (CW == 8)
+            lds_wait<younger>(buf[ch % 2][0], buf[ch % 2][1], buf[ch % 2][2], buf[ch % 2][3]);
+          else
+            lds_wait<younger>(buf[ch % 2][0], buf[ch % 2][1]);
+          sfor<0, CW>([&](auto ic) __attribute__((always_inline)) {
             constexpr int i = decltype(ic)::value;
-            constexpr int j = JA + 8 * ch + i;
+            constexpr int j = JA + CW * ch + i;
             if constexpr (j > k && j < NV) {
               const double cv = (i & 1) ? buf[ch % 2][i / 2].y : buf[ch % 2][i / 2].x;
               Rg[j] = fma(nt, cv, Rg[j]);
@@ -923,6 +956,12 @@ solve_kernel(SolveArgs a) {
   }
   HMPC_STAMP(6);
 
+  // stage / component of my variable, recomputed from an opaque thread id:
+  // phase 3's copies would stay alive (spilled) across the factorisation
+  const int tid_o = tid + opaque_zero();
+  const int vj = (tid_o * 43) >> 8;   // tid / 6 for tid < 128
+  const int vc = tid_o - 6 * vj;
+
   // ---------------- phase 6: Goldfarb-Idnani, range-space form --------------
   // Constraints owned by lane v (id = 4 v + slot), all as n'v >= b:
   //   c in 3..5 : slot0  v >= -lim,  slot1 -v >= -lim          (:123-128)
@@ -955,7 +994,17 @@ solve_kernel(SolveArgs a) {
     }
     znorm = sqrt(s2);
   }
-  const double fric_norm = sqrt(1.0 + mu * mu);
+  // slot 0/1 coefficients of my constraints (see the table above)
+  double a0 = 1.0, muf = 0.0, k0 = 0.0, k1 = 0.0, inv01 = 1.0;
+  if (vc >= 3) {
+    k0 = k1 = tau_lim(vc);
+  } else if (vc == 2) {
+    k1 = kFzMax;
+  } else {
+    a0 = -1.0;
+    muf = mu;
+    inv01 = 1.0 / sqrt(1.0 + mu * mu);
+  }
   int actmask = 0;
 
   double* Rm = sm + L::RM;   // packed upper, column k at loff(k)
@@ -1003,35 +1052,27 @@ solve_kernel(SolveArgs a) {
     // ---- slacks of my constraints; pick the most violated ----
     xs[tid] = v;
     B::sync();
+    // branch-free: slots 0/1 are +-a0 v + muf fz_stage + k0/k1; slot 2 the
+    // z row ZB_k + zc ((k-1) S1 - S2) with S1 = sum C_j fz_j, S2 = sum j C_j fz_j
+    // over j <= k-2 (prefix sums over a uniform trip count)
+    double z1 = 0.0, z2 = 0.0;
+    sfor<0, (N > 2 ? N - 2 : 0)>([&](auto jc) __attribute__((always_inline)) {
+      constexpr int j = decltype(jc)::value;
+      const double val = sm[L::CC + j] * xs[6 * j + 2];
+      const double msk = (j <= vj - 2) ? 1.0 : 0.0;
+      z1 = fma(msk, val, z1);
+      z2 = fma(msk * (double)j, val, z2);
+    });
+    const double fzs = xs[6 * (active_lane ? vj : 0) + 2];
+    const double sc0 = fma(a0, v, fma(muf, fzs, k0)) * inv01;
+    const double sc1 = fma(-a0, v, fma(muf, fzs, k1)) * inv01;
+    const double zrow = (sm[L::ZB + (active_lane ? vj : 0)] - kZmin) + zc * fma((double)(vj - 1), z1, -z2);
+    const double sc2 = znorm > 0.0 ? zrow / znorm : ((zrow < -kTol) ? -INFINITY : INFINITY);
     double best = INFINITY;
     int bid = 0x7fffffff;
-    for (int sl = 0; sl < nslots; ++sl) {
-      if (actmask & (1 << sl)) continue;
-      double s, nrm;
-      if (vc >= 3) {
-        if (sl < 2) {
-          s = (sl == 0 ? v : -v) + tau_lim(vc);
-          nrm = 1.0;
-        } else {
-          double z = sm[L::ZB + vj];
-          for (int j = 0; j <= vj - 2; ++j)
-            if (sm[L::CC + j] != 0.0) z += zc * (double)(vj - 1 - j) * xs[6 * j + 2];
-          s = z - kZmin;
-          nrm = znorm;
-        }
-      } else if (vc == 2) {
-        s = sl == 0 ? v : kFzMax - v;
-        nrm = 1.0;
-      } else {
-        const double fz = xs[6 * vj + 2];
-        s = (sl == 0 ? -v : v) + mu * fz;
-        nrm = fric_norm;
-      }
-      double sc;
-      if (nrm > 0.0) sc = s / nrm;
-      else sc = (s < -kTol) ? -INFINITY : INFINITY;
-      argmin_combine(best, bid, sc, 4 * tid + sl);
-    }
+    if (nslots > 0 && !(actmask & 1)) argmin_combine(best, bid, sc0, 4 * tid);
+    if (nslots > 1 && !(actmask & 2)) argmin_combine(best, bid, sc1, 4 * tid + 1);
+    if (nslots > 2 && !(actmask & 4)) argmin_combine(best, bid, sc2, 4 * tid + 2);
     B::argmin(best, bid, red);
     if (!(best < -kTol)) break;   // primal feasible: optimal
     const int p = uni(bid);
@@ -1163,61 +1204,55 @@ solve_kernel(SolveArgs a) {
   HMPC_STAMP(7);
 
   // ---------------- phase 7: outputs ----------------------------------------
+  // u* straight out; x* by a lane-parallel forward simulation (lane r < 12
+  // holds x[r]) written as it goes; the objective as a per-lane sum + one
+  // reduction.
   if (active_lane) a.u[b * NV + tid] = v;
   xs[tid] = v;
-  __syncthreads();   // L is dead: XO aliases it
+  B::sync();
   {
-    double* xo = sm + L::XO;
-    double x[12];
-#pragma unroll
-    for (int r = 0; r < 12; ++r) x[r] = sm[L::XIN + r];
-    if (tid < 12) xo[tid] = sm[L::XIN + tid];
-    double objv = 0.0;
-    const double* xr = a.x_ref + b * 12 * N;
+#ifndef HMPC_STAMPS
+    double* xg = a.x ? a.x + b * 12 * (N + 1) : nullptr;
+#else
+    double* xg = nullptr;
+#endif
+    double xr = tid < 12 ? sm[L::XIN + tid] : 0.0;
+    if (xg && tid < 12) xg[tid] = xr;
+    const double qr = qdiag(tid);
+    const double* xrf = a.x_ref + b * 12 * N;
+    const int rw = (tid >= 9 && tid < 12) ? tid - 9 : 0;   // my row of Bd's omega block
+    const int rv = (tid >= 6 && tid < 9) ? tid - 6 : 0;    // my row of Bd's velocity block
+    double objl = 0.0;
 #pragma unroll 1
     for (int k = 0; k < N; ++k) {
       const double cp = sm[L::CS + 2 * k], sp = sm[L::CS + 2 * k + 1];
-      const double* bw = sm + L::BW + 18 * k;
-      double u[6];
+      const double* bwr = sm + L::BW + 18 * k + 6 * rw;
+      const double* uk = xs + 6 * k;
+      double bw_u = 0.0;
 #pragma unroll
-      for (int c = 0; c < 6; ++c) u[c] = xs[6 * k + c];
-      ad_times(x, dt, cp, sp);
-#pragma unroll
-      for (int r = 0; r < 3; ++r) {
-        double acc = 0.0;
-#pragma unroll
-        for (int c = 0; c < 3; ++c) acc = fma(bv<VAR>(r, c, dtm, cp, sp), u[c], acc);
-        x[6 + r] += acc;
-        double acw = 0.0;
-#pragma unroll
-        for (int c = 0; c < 6; ++c) acw = fma(bw[6 * r + c], u[c], acw);
-        x[9 + r] += acw;
+      for (int c = 0; c < 6; ++c) bw_u = fma(bwr[c], uk[c], bw_u);
+      double bv_u = 0.0;
+      if constexpr (VAR == 3) {
+        bv_u = dtm * uk[rv];
+      } else {   // Rz' dt/m
+        const double u0 = uk[0], u1 = uk[1], u2 = uk[2];
+        bv_u = (rv == 0) ? dtm * (cp * u0 - sp * u1) : ((rv == 1) ? dtm * (sp * u0 + cp * u1) : dtm * u2);
       }
-      x[8] += -a.g * dt;
+      const double bu = (tid >= 9 && tid < 12) ? bw_u : ((tid >= 6 && tid < 9) ? bv_u : 0.0);
+      xr = ad_lane(xr, dt, cp, sp) + bu + ((tid == 8) ? -a.g * dt : 0.0);
       const double kf = (k == N - 1) ? kTermQ : 1.0;
-#pragma unroll
-      for (int r = 0; r < 12; ++r) {
-        const double e = x[r] - xr[12 * k + r];
-        objv = fma(kf * kQ[r] * e, e, objv);
-      }
-      if (k < N - 1) {
+      const double e = xr - (tid < 12 ? xrf[12 * k + tid] : 0.0);
+      objl = fma(kf * qr * e, e, objl);
+      if (k < N - 1 && tid < 6) {
         const double ub = a.uref_aliased ? ubar_z_alias
                                          : ((sm[L::CC + k] != 0.0) ? 2.0 * a.m * a.g : 0.0);
-#pragma unroll
-        for (int c = 0; c < 6; ++c) {
-          const double du = u[c] - (c == 2 ? ub : 0.0);
-          objv = fma(kRdiag * du, du, objv);
-        }
+        const double du = uk[tid] - (tid == 2 ? ub : 0.0);
+        objl = fma(kRdiag * du, du, objl);
       }
-      if (tid == 0)
-#pragma unroll
-        for (int r = 0; r < 12; ++r) xo[12 * (k + 1) + r] = x[r];
+      if (xg && tid < 12) xg[12 * (k + 1) + tid] = xr;
     }
-    __syncthreads();
-#ifndef HMPC_STAMPS
-    if (a.x)
-      for (int i = tid; i < 12 * (N + 1); i += NT) a.x[b * 12 * (N + 1) + i] = xo[i];
-#else
+    const double objv = B::sum(objl, red);
+#ifdef HMPC_STAMPS
     HMPC_STAMP(8);
     if (a.x && tid == 0)
       for (int i = 0; i < 12; ++i)
