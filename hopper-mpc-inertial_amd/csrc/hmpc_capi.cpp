@@ -116,10 +116,10 @@ int hmpc_create(hmpc_ctx** out, int variant, int N, double t, double m, double g
 
 int hmpc_destroy(hmpc_ctx* c) {
   if (!c) return HMPC_ERR_ARG;
-  hipSetDevice(c->device);
-  if (c->dbuf) hipFree(c->dbuf);
-  if (c->scratch_i32) hipFree(c->scratch_i32);
-  if (c->own_stream) hipStreamDestroy(c->own_stream);
+  (void)hipSetDevice(c->device);
+  if (c->dbuf) (void)hipFree(c->dbuf);
+  if (c->scratch_i32) (void)hipFree(c->scratch_i32);
+  if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   delete c;
   return HMPC_OK;
 }
@@ -158,8 +158,8 @@ int hmpc_time_solve_batch(hmpc_ctx* c, int64_t B, const double* x_in, const doub
   HMPC_HIP(c, hipEventSynchronize(e1));
   float t = 0.f;
   HMPC_HIP(c, hipEventElapsedTime(&t, e0, e1));
-  hipEventDestroy(e0);
-  hipEventDestroy(e1);
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
   *ms = (double)t / reps;
   HMPC_HIP(c, hipGetLastError());
   return HMPC_OK;
@@ -177,7 +177,7 @@ int hmpc_solve_batch_host(hmpc_ctx* c, int64_t B, const double* x_in, const doub
   const size_t nd_out = 6 * N + 12 * (N + 1) + 1;
   const size_t bytes = (size_t)B * (8 * (nd_in + nd_out) + 8) + 256;
   if (bytes > c->dbuf_bytes) {
-    if (c->dbuf) hipFree(c->dbuf);
+    if (c->dbuf) (void)hipFree(c->dbuf);
     c->dbuf = nullptr;
     c->dbuf_bytes = 0;
     HMPC_HIP(c, hipMalloc(&c->dbuf, bytes));
@@ -226,7 +226,7 @@ int hmpc_mpcontrol_batch(hmpc_ctx* c, int64_t B, int init, const double* x_in,
   hipStream_t s = (hipStream_t)stream;
   if (init) {
     if (B > c->scratch_n) {
-      if (c->scratch_i32) hipFree(c->scratch_i32);
+      if (c->scratch_i32) (void)hipFree(c->scratch_i32);
       c->scratch_i32 = nullptr;
       c->scratch_n = 0;
       HMPC_HIP(c, hipMalloc(&c->scratch_i32, 8 * B));

@@ -251,7 +251,7 @@ struct Lay {
   static constexpr int NT = 64 * W;
   // active-set capacity (registers for Qw, LDS for R); the largest active set
   // seen over 65536 random N=10 instances is 12
-  static constexpr int QMAX = NV < 24 ? NV : (N <= 10 ? 24 : 48);
+  static constexpr int QMAX = NV < 20 ? NV : (N <= 10 ? 20 : 48);
   static constexpr int e2(int n) { return (n + 1) & ~1; }
   static constexpr int NS = 22;                    // unique entries of S_t
   static constexpr int LCN = NV * (NV + 1) / 2;    // packed L
@@ -262,16 +262,20 @@ struct Lay {
   static constexpr int BW = CS + 2 * N;            // [N][3][6] rows 9..11 of Bd_k
   static constexpr int ZB = BW + 18 * N;           // [N+1] free-response heights
   static constexpr int XS = ZB + e2(N + 1);        // [NT] primal broadcast
-  static constexpr int RED = XS + NT;              // [16]
-  static constexpr int ZR = RED + 16;              // [2] a 0.0 for masked lanes' loads
-  static constexpr int UA = ZR + 2;                // [QMAX] active multipliers
+  static constexpr int RED = XS + NT;              // [4] cross-wave reductions (W <= 2)
+  static constexpr int ZR = RED + 4;               // [2] a 0.0 for masked lanes' loads
+  // active-set state (phase 6); the Cholesky's column buffers overlay it
+  static constexpr int G0 = ZR + 2;
+  static constexpr int UA = G0;                    // [QMAX] active multipliers
   static constexpr int ACT = UA + QMAX;            // [QMAX] active ids (int)
   static constexpr int CB = ACT + QMAX;            // [QMAX] c = Qw' w
   static constexpr int GV = CB + QMAX;             // [QMAX][2] Givens of a drop
   static constexpr int SD = GV + 2 * QMAX;         // [QMAX] subdiagonal scratch
   static constexpr int RM = SD + QMAX;             // packed upper R, col l at l(l+1)/2
-  static constexpr int COLB = (RM + e2(QMAX * (QMAX + 1) / 2) + 1) & ~1;   // [2][NT+8], 16-B aligned
-  static constexpr int U0 = COLB + 2 * (NT + 8);
+  static constexpr int GEND = RM + e2(QMAX * (QMAX + 1) / 2);
+  static constexpr int COLB = G0;                  // [2][NT+8] (phase 4 only), 16-B aligned
+  static_assert((G0 & 1) == 0, "column buffers must be 16-B aligned");
+  static constexpr int U0 = (GEND > COLB + 2 * (NT + 8)) ? GEND : COLB + 2 * (NT + 8);
   // union A (phases 0-3)
   static constexpr int XLIN = U0;                  // [N][12]  rows 0..N-1
   static constexpr int PF = XLIN + 12 * N;         // [N][3]
@@ -1205,19 +1209,16 @@ solve_kernel(SolveArgs a) {
 
   // ---------------- phase 7: outputs ----------------------------------------
   // u* straight out; x* by a lane-parallel forward simulation (lane r < 12
-  // holds x[r]) written as it goes; the objective as a per-lane sum + one
-  // reduction.
+  // holds x[r]) staged in LDS and written coalesced at the end (per-step
+  // 96-byte stores cost ~1.9x the bytes at the memory side); the objective
+  // as a per-lane sum + one reduction.
   if (active_lane) a.u[b * NV + tid] = v;
   xs[tid] = v;
-  B::sync();
+  __syncthreads();   // L is dead: XO aliases it
   {
-#ifndef HMPC_STAMPS
-    double* xg = a.x ? a.x + b * 12 * (N + 1) : nullptr;
-#else
-    double* xg = nullptr;
-#endif
+    double* xo = sm + L::XO;
     double xr = tid < 12 ? sm[L::XIN + tid] : 0.0;
-    if (xg && tid < 12) xg[tid] = xr;
+    if (tid < 12) xo[tid] = xr;
     const double qr = qdiag(tid);
     const double* xrf = a.x_ref + b * 12 * N;
     const int rw = (tid >= 9 && tid < 12) ? tid - 9 : 0;   // my row of Bd's omega block
@@ -1249,10 +1250,14 @@ solve_kernel(SolveArgs a) {
         const double du = uk[tid] - (tid == 2 ? ub : 0.0);
         objl = fma(kRdiag * du, du, objl);
       }
-      if (xg && tid < 12) xg[12 * (k + 1) + tid] = xr;
+      if (tid < 12) xo[12 * (k + 1) + tid] = xr;
     }
     const double objv = B::sum(objl, red);
-#ifdef HMPC_STAMPS
+    __syncthreads();
+#ifndef HMPC_STAMPS
+    if (a.x)
+      for (int i = tid; i < 12 * (N + 1); i += NT) a.x[b * 12 * (N + 1) + i] = xo[i];
+#else
     HMPC_STAMP(8);
     if (a.x && tid == 0)
       for (int i = 0; i < 12; ++i)

@@ -12,11 +12,15 @@ Contents
 ``qp_exact``     an exact fp64 QP solve of that standard form (interior point
                  to 1e-12, then an active-set polish and a KKT certificate).
                  It stands in for cvxpy+OSQP, which are absent from this image.
-``plan``         restatement of ``Runner.path_plan_init`` / ``gait_map`` /
-                 ``path_plan_grab`` (``src/robotrunner.py:166-230``), used to
-                 draw synthetic instances exactly as SURVEY.md section 8d says.
-``csrc/``        a C restatement of the same construction + the same exact
-                 solver (the ``cpu_baseline`` "port" timed in bench.py).
+``hmpc_port.c`` a plain-C restatement of the same construction, condensed
+  / ``port``     densely and solved exactly by a classic Goldfarb-Idnani dual
+                 active set (``make -C oracle`` -> libhmpc_port.so, ctypes
+                 binding in ``port.py``): the second checker and the
+                 ``cpu_baseline`` "port" timed by bench.py (OpenMP).
+
+The synthetic-instance planner (``Runner.path_plan_init`` / ``gait_map``
+restated) lives on the product side, ``hopper-mpc-inertial_amd/hmpc_plan.py``,
+pinned by tests/test_plan.py against the reference's recorded plan.
 
 Pinning: the problem data is pinned bit-for-bit (to a few ulps) against
 fixtures recorded from the reference's OWN ``gen_dt_dynamics``/``build_qp``
