@@ -536,6 +536,7 @@ solve_kernel(SolveArgs a) {
   using B = Blk<W>;
   __shared__ __attribute__((aligned(16))) double sm[L::TOTAL];
   double* red = sm + L::RED;
+  double* xs = sm + L::XS;
 #ifdef HMPC_STAMPS
   long long stamp_[16] = {0};
 #endif
@@ -544,7 +545,6 @@ solve_kernel(SolveArgs a) {
   const int tid = threadIdx.x;
   const int64_t b = blockIdx.x;
   const double dt = a.dt;
-  const double mu = a.mu ? a.mu[b] : a.mu_default;
   const double dtm = dt / a.m;
 
   // ---------------- phase 0: coalesced loads --------------------------------
@@ -799,6 +799,7 @@ solve_kernel(SolveArgs a) {
       hv = 2.0 * hacc - 2.0 * Vj * ub;
     }
   }
+  xs[tid] = hv;      // parked in LDS across the factorisation
   __syncthreads();   // union A (XLIN/XREF/PF/S/DG) is dead from here on
   HMPC_STAMP(4);
 
@@ -955,11 +956,15 @@ solve_kernel(SolveArgs a) {
   // ---------------- phase 5: v0 = -L^-T L^-1 h -------------------------------
   double v = 0.0;
   {
-    const double y = tri_fwd<N>(-hv, Rg, dinv, red);
+    const double y = tri_fwd<N>(-xs[tid], Rg, dinv, red);
     v = tri_bwd<N>(y, Lc, zero, dinv, red);
   }
   HMPC_STAMP(6);
 
+  // per-instance scalars needed after the factorisation are re-derived here
+  // rather than kept live across it (they were spilled there)
+  const double mu = a.mu ? a.mu[b] : a.mu_default;
+  const double dtm2 = dt / a.m + 0.0 * (double)opaque_zero();
   // stage / component of my variable, recomputed from an opaque thread id:
   // phase 3's copies would stay alive (spilled) across the factorisation
   const int tid_o = tid + opaque_zero();
@@ -979,7 +984,7 @@ solve_kernel(SolveArgs a) {
   if (zmin_gap_k0 < -kTol || zmin_gap_k1 < -kTol) status = ST_INFEAS;
   // coefficient of fz_j in z_k (j <= k-2): dt * (dt/m) * (k-1-j), stance only
   // (Bd[8][2] = dt/m in both variants)
-  const double zc = dt * dtm;
+  const double zc = dt * dtm2;
 
   const bool stance_me = active_lane && vc <= 2 && sm[L::CC + vj] != 0.0;
   int nslots = 0;
@@ -1017,7 +1022,6 @@ solve_kernel(SolveArgs a) {
   double* cbv = sm + L::CB;
   double* gv = sm + L::GV;
   double* sdg = sm + L::SD;
-  double* xs = sm + L::XS;
   double Qw[QMAX];   // row `tid` of the orthonormal basis of L^-1 N_A
 #pragma unroll
   for (int l = 0; l < QMAX; ++l) Qw[l] = 0.0;
@@ -1219,7 +1223,7 @@ solve_kernel(SolveArgs a) {
     double* xo = sm + L::XO;
     double xr = tid < 12 ? sm[L::XIN + tid] : 0.0;
     if (tid < 12) xo[tid] = xr;
-    const double qr = qdiag(tid);
+    const double qr = qdiag(tid_o);   // (not CSE-d with phase 2's copy)
     const double* xrf = a.x_ref + b * 12 * N;
     const int rw = (tid >= 9 && tid < 12) ? tid - 9 : 0;   // my row of Bd's omega block
     const int rv = (tid >= 6 && tid < 9) ? tid - 6 : 0;    // my row of Bd's velocity block
@@ -1234,10 +1238,10 @@ solve_kernel(SolveArgs a) {
       for (int c = 0; c < 6; ++c) bw_u = fma(bwr[c], uk[c], bw_u);
       double bv_u = 0.0;
       if constexpr (VAR == 3) {
-        bv_u = dtm * uk[rv];
+        bv_u = dtm2 * uk[rv];
       } else {   // Rz' dt/m
         const double u0 = uk[0], u1 = uk[1], u2 = uk[2];
-        bv_u = (rv == 0) ? dtm * (cp * u0 - sp * u1) : ((rv == 1) ? dtm * (sp * u0 + cp * u1) : dtm * u2);
+        bv_u = (rv == 0) ? dtm2 * (cp * u0 - sp * u1) : ((rv == 1) ? dtm2 * (sp * u0 + cp * u1) : dtm2 * u2);
       }
       const double bu = (tid >= 9 && tid < 12) ? bw_u : ((tid >= 6 && tid < 9) ? bv_u : 0.0);
       xr = ad_lane(xr, dt, cp, sp) + bu + ((tid == 8) ? -a.g * dt : 0.0);
@@ -1245,7 +1249,7 @@ solve_kernel(SolveArgs a) {
       const double e = xr - (tid < 12 ? xrf[12 * k + tid] : 0.0);
       objl = fma(kf * qr * e, e, objl);
       if (k < N - 1 && tid < 6) {
-        const double ub = a.uref_aliased ? ubar_z_alias
+        const double ub = a.uref_aliased ? ((sm[L::CC + N - 1] != 0.0) ? 2.0 * a.m * a.g : 0.0)
                                          : ((sm[L::CC + k] != 0.0) ? 2.0 * a.m * a.g : 0.0);
         const double du = uk[tid] - (tid == 2 ? ub : 0.0);
         objl = fma(kRdiag * du, du, objl);
