@@ -58,6 +58,10 @@ hmpc::SolveArgs make_args(hmpc_ctx* c, int64_t B, const double* x_in, const doub
   memcpy(a.rh, c->rh, sizeof(a.rh));
   a.uref_aliased = c->uref_mode == HMPC_UREF_ALIASED ? 1 : 0;
   a.shift_mode = shift_mode;
+  const int N = c->N;
+  a.xref_bs = 12 * (int64_t)N; a.xref_rs = 12;
+  a.pf_bs = 3 * (int64_t)N; a.pf_rs = 3;
+  a.C_bs = N;
   return a;
 }
 
@@ -216,14 +220,25 @@ int hmpc_solve_batch_host(hmpc_ctx* c, int64_t B, const double* x_in, const doub
   return HMPC_OK;
 }
 
-int hmpc_mpcontrol_batch(hmpc_ctx* c, int64_t B, int init, const double* x_in,
-                         const double* x_ref, const double* pf, const double* C,
-                         const double* mu, double* x_prev, double* u, double* obj,
-                         int32_t* status, int32_t* iters, void* stream) {
-  int rc = check_solve_args(c, B, x_in, x_prev, x_ref, pf, C, u, status);
-  if (rc != HMPC_OK || B == 0) return rc;
+namespace {
+
+// Mpc.mpcontrol (src/mpc_cvx_euler_3f.py:41-69) for B instances; `view`
+// carries the x_ref / pf / C strides (contiguous or a resident plan).
+int mpcontrol_impl(hmpc_ctx* c, int64_t B, int init, const double* x_in, const double* x_ref,
+                   const double* pf, const double* C, const double* mu, double* x_prev,
+                   double* u, double* obj, int32_t* status, int32_t* iters, void* stream,
+                   const hmpc::SolveArgs* view) {
   HMPC_HIP(c, hipSetDevice(c->device));
   hipStream_t s = (hipStream_t)stream;
+  auto args = [&](int32_t* st, int32_t* it, double* ob, int mode) {
+    hmpc::SolveArgs a = make_args(c, B, x_in, x_prev, x_ref, pf, C, mu, u, x_prev, ob, st, it, mode);
+    if (view) {
+      a.xref_bs = view->xref_bs; a.xref_rs = view->xref_rs;
+      a.pf_bs = view->pf_bs; a.pf_rs = view->pf_rs;
+      a.C_bs = view->C_bs;
+    }
+    return a;
+  };
   if (init) {
     if (B > c->scratch_n) {
       if (c->scratch_i32) (void)hipFree(c->scratch_i32);
@@ -235,23 +250,91 @@ int hmpc_mpcontrol_batch(hmpc_ctx* c, int64_t B, int init, const double* x_in,
     int32_t* s1 = c->scratch_i32;
     int32_t* i1 = c->scratch_i32 + B;
     // pass 1: linearise about [x_in; x_ref]  (src/mpc_cvx_euler_3f.py:50-58)
-    hmpc::SolveArgs a1 = make_args(c, B, x_in, x_prev, x_ref, pf, C, mu, u, x_prev, nullptr, s1,
-                                   i1, 1);
-    if (!hmpc::launch_solve(c->variant, c->N, a1, s)) return HMPC_ERR_UNSUPPORTED;
+    if (!hmpc::launch_solve(c->variant, c->N, args(s1, i1, nullptr, 1), s)) return HMPC_ERR_UNSUPPORTED;
     // pass 2: linearise about x* of pass 1 (in place: each workgroup stages
     // its x_lin in LDS before writing x*)
-    hmpc::SolveArgs a2 = make_args(c, B, x_in, x_prev, x_ref, pf, C, mu, u, x_prev, obj, status,
-                                   iters, 0);
-    hmpc::launch_solve(c->variant, c->N, a2, s);
+    hmpc::launch_solve(c->variant, c->N, args(status, iters, obj, 0), s);
     const int tpb = 256;
     hipLaunchKernelGGL(combine_status, dim3((unsigned)((B + tpb - 1) / tpb)), dim3(tpb), 0, s, B,
                        s1, i1, status, iters);
   } else {
     // time shift of the previous x*  (src/mpc_cvx_euler_3f.py:59-62)
-    hmpc::SolveArgs a = make_args(c, B, x_in, x_prev, x_ref, pf, C, mu, u, x_prev, obj, status,
-                                  iters, 2);
-    if (!hmpc::launch_solve(c->variant, c->N, a, s)) return HMPC_ERR_UNSUPPORTED;
+    if (!hmpc::launch_solve(c->variant, c->N, args(status, iters, obj, 2), s)) return HMPC_ERR_UNSUPPORTED;
   }
+  HMPC_HIP(c, hipGetLastError());
+  return HMPC_OK;
+}
+
+}  // namespace
+
+int hmpc_mpcontrol_batch(hmpc_ctx* c, int64_t B, int init, const double* x_in,
+                         const double* x_ref, const double* pf, const double* C,
+                         const double* mu, double* x_prev, double* u, double* obj,
+                         int32_t* status, int32_t* iters, void* stream) {
+  int rc = check_solve_args(c, B, x_in, x_prev, x_ref, pf, C, u, status);
+  if (rc != HMPC_OK || B == 0) return rc;
+  return mpcontrol_impl(c, B, init, x_in, x_ref, pf, C, mu, x_prev, u, obj, status, iters, stream,
+                        nullptr);
+}
+
+int hmpc_mpcontrol_plan_batch(hmpc_ctx* c, int64_t B, int init, const double* x_in,
+                              const double* x_ref_plan, const double* pf_plan, int64_t T,
+                              int64_t plan_bstride, int64_t k, int mpc_factor, const double* C,
+                              int64_t C_bstride, const double* mu, double* x_prev, double* u,
+                              double* obj, int32_t* status, int32_t* iters, void* stream) {
+  int rc = check_solve_args(c, B, x_in, x_prev, x_ref_plan, pf_plan, C, u, status);
+  if (rc != HMPC_OK || B == 0) return rc;
+  const int N = c->N;
+  if (mpc_factor <= 0 || k < 0 || T <= 0 || k + (int64_t)(N - 1) * mpc_factor >= T) {
+    c->err = "plan window k + (N-1)*mpc_factor outside [0, T)";
+    return HMPC_ERR_ARG;
+  }
+  if (plan_bstride != 0 && plan_bstride < T) {
+    c->err = "plan_bstride must be 0 (shared plan) or >= T";
+    return HMPC_ERR_ARG;
+  }
+  if (C_bstride != 0 && C_bstride < N) {
+    c->err = "C_bstride must be 0 (shared schedule) or >= N";
+    return HMPC_ERR_ARG;
+  }
+  if ((int64_t)mpc_factor * 12 > 0x7fffffff / 2) { c->err = "mpc_factor too large"; return HMPC_ERR_ARG; }
+  hmpc::SolveArgs view;
+  view.xref_bs = 12 * plan_bstride; view.xref_rs = 12 * mpc_factor;
+  view.pf_bs = 3 * plan_bstride; view.pf_rs = 3 * mpc_factor;
+  view.C_bs = C_bstride;
+  return mpcontrol_impl(c, B, init, x_in, x_ref_plan + 12 * k, pf_plan + 3 * k, C, mu, x_prev, u,
+                        obj, status, iters, stream, &view);
+}
+
+int hmpc_plant_batch(hmpc_ctx* c, int64_t B, int n_steps, double dt, const double* J, double* X,
+                     const double* U, int64_t U_bstride, const double* pf, int64_t pf_bstride,
+                     int64_t pf_sstride, double* X_hist, double* x_out, void* stream) {
+  if (!c) return HMPC_ERR_ARG;
+  if (B < 0 || n_steps < 0 || !(dt > 0.0)) { c->err = "B < 0, n_steps < 0 or dt <= 0"; return HMPC_ERR_ARG; }
+  if (B == 0) return HMPC_OK;
+  if (!J || !X || !U || !pf) { c->err = "null pointer"; return HMPC_ERR_ARG; }
+  if (U_bstride < 0 || pf_bstride < 0 || pf_sstride < 0) { c->err = "negative stride"; return HMPC_ERR_ARG; }
+  HMPC_HIP(c, hipSetDevice(c->device));
+  hmpc::PlantArgs a;
+  a.B = B; a.n_steps = n_steps; a.dt = dt; a.m = c->m; a.g = c->g;
+  memcpy(a.J, J, sizeof(a.J));
+  memcpy(a.Jinv, c->Jinv, sizeof(a.Jinv));
+  memcpy(a.rh, c->rh, sizeof(a.rh));
+  a.X = X; a.U = U; a.U_bs = U_bstride;
+  a.pf = pf; a.pf_bs = pf_bstride; a.pf_ss = pf_sstride;
+  a.X_hist = X_hist; a.x_out = x_out;
+  hmpc::launch_plant(a, (hipStream_t)stream);
+  HMPC_HIP(c, hipGetLastError());
+  return HMPC_OK;
+}
+
+int hmpc_convert_batch(hmpc_ctx* c, int64_t B, const double* X, double* x, void* stream) {
+  if (!c) return HMPC_ERR_ARG;
+  if (B < 0) { c->err = "B < 0"; return HMPC_ERR_ARG; }
+  if (B == 0) return HMPC_OK;
+  if (!X || !x) { c->err = "null pointer"; return HMPC_ERR_ARG; }
+  HMPC_HIP(c, hipSetDevice(c->device));
+  hmpc::launch_convert(B, X, x, (hipStream_t)stream);
   HMPC_HIP(c, hipGetLastError());
   return HMPC_OK;
 }

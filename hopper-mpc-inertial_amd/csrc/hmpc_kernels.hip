@@ -548,15 +548,25 @@ solve_kernel(SolveArgs a) {
   const double dtm = dt / a.m;
 
   // ---------------- phase 0: coalesced loads --------------------------------
+  // x_ref / pf / C may be strided views (a resident plan, path_plan_grab
+  // src/robotrunner.py:228-230: rows k, k+f, ...; batch stride 0 = shared)
+  const double* xrf = a.x_ref + b * a.xref_bs;
   for (int i = tid; i < 12; i += NT) sm[L::XIN + i] = a.x_in[b * 12 + i];
-  for (int i = tid; i < 12 * N; i += NT) sm[L::XREF + i] = a.x_ref[b * 12 * N + i];
-  for (int i = tid; i < 3 * N; i += NT) sm[L::PF + i] = a.pf[b * 3 * N + i];
-  for (int i = tid; i < N; i += NT) sm[L::CC + i] = a.C[b * N + i];
+  for (int i = tid; i < 12 * N; i += NT) {
+    const int r = i / 12, c = i - 12 * r;
+    sm[L::XREF + i] = xrf[r * a.xref_rs + c];
+  }
+  for (int i = tid; i < 3 * N; i += NT) {
+    const int r = i / 3, c = i - 3 * r;
+    sm[L::PF + i] = a.pf[b * a.pf_bs + r * a.pf_rs + c];
+  }
+  for (int i = tid; i < N; i += NT) sm[L::CC + i] = a.C[b * a.C_bs + i];
   if (a.shift_mode == 0) {
     for (int i = tid; i < 12 * N; i += NT) sm[L::XLIN + i] = a.x_lin[b * 12 * (N + 1) + i];
   } else if (a.shift_mode == 1) {   // [x_in; x_ref]          (3f :52-53)
+    __syncthreads();
     for (int i = tid; i < 12 * N; i += NT)
-      sm[L::XLIN + i] = i < 12 ? a.x_in[b * 12 + i] : a.x_ref[b * 12 * N + i - 12];
+      sm[L::XLIN + i] = i < 12 ? sm[L::XIN + i] : sm[L::XREF + i - 12];
   } else {                          // [x_in; x_prev[2:]; x_prev[N]]  (3f :59-62)
     const double* xp = a.x_lin + b * 12 * (N + 1);
     for (int i = tid; i < 12 * N; i += NT) {
@@ -1224,7 +1234,7 @@ solve_kernel(SolveArgs a) {
     double xr = tid < 12 ? sm[L::XIN + tid] : 0.0;
     if (tid < 12) xo[tid] = xr;
     const double qr = qdiag(tid_o);   // (not CSE-d with phase 2's copy)
-    const double* xrf = a.x_ref + b * 12 * N;
+    const double* xrf = a.x_ref + b * a.xref_bs;
     const int rw = (tid >= 9 && tid < 12) ? tid - 9 : 0;   // my row of Bd's omega block
     const int rv = (tid >= 6 && tid < 9) ? tid - 6 : 0;    // my row of Bd's velocity block
     double objl = 0.0;
@@ -1246,7 +1256,7 @@ solve_kernel(SolveArgs a) {
       const double bu = (tid >= 9 && tid < 12) ? bw_u : ((tid >= 6 && tid < 9) ? bv_u : 0.0);
       xr = ad_lane(xr, dt, cp, sp) + bu + ((tid == 8) ? -a.g * dt : 0.0);
       const double kf = (k == N - 1) ? kTermQ : 1.0;
-      const double e = xr - (tid < 12 ? xrf[12 * k + tid] : 0.0);
+      const double e = xr - (tid < 12 ? xrf[k * a.xref_rs + tid] : 0.0);
       objl = fma(kf * qr * e, e, objl);
       if (k < N - 1 && tid < 6) {
         const double ub = a.uref_aliased ? ((sm[L::CC + N - 1] != 0.0) ? 2.0 * a.m * a.g : 0.0)

@@ -36,6 +36,14 @@ SIGNATURES = {
     'hmpc_solve_batch': (ctypes.c_int, [_VP, ctypes.c_int64] + [_VP] * 11 + [_VP]),
     'hmpc_solve_batch_host': (ctypes.c_int, [_VP, ctypes.c_int64] + [_VP] * 11),
     'hmpc_mpcontrol_batch': (ctypes.c_int, [_VP, ctypes.c_int64, ctypes.c_int] + [_VP] * 10 + [_VP]),
+    'hmpc_mpcontrol_plan_batch': (ctypes.c_int, [_VP, ctypes.c_int64, ctypes.c_int, _VP, _VP, _VP,
+                                                 ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
+                                                 ctypes.c_int, _VP, ctypes.c_int64]
+                                  + [_VP] * 6 + [_VP]),
+    'hmpc_plant_batch': (ctypes.c_int, [_VP, ctypes.c_int64, ctypes.c_int, ctypes.c_double, _D, _VP,
+                                        _VP, ctypes.c_int64, _VP, ctypes.c_int64, ctypes.c_int64,
+                                        _VP, _VP, _VP]),
+    'hmpc_convert_batch': (ctypes.c_int, [_VP, ctypes.c_int64, _VP, _VP, _VP]),
     'hmpc_last_error': (ctypes.c_char_p, [_VP]),
     'hmpc_time_solve_batch': (ctypes.c_int, [_VP, ctypes.c_int64] + [_VP] * 11
                               + [ctypes.c_int, _VP, ctypes.POINTER(ctypes.c_double)]),
@@ -186,6 +194,64 @@ class Context:
                                             ctypes.c_void_p(s))
         self._check(rc, 'hmpc_mpcontrol_batch')
         return out
+
+    def mpcontrol_plan_device(self, init, x_in, x_ref_plan, pf_plan, k, mpc_factor, C, x_prev,
+                              mu=None, out=None, stream=None):
+        """The Runner's ``mpcontrol`` call (src/robotrunner.py:98-107) for B
+        robots, reading path_plan_grab(plan, k) in place from a device plan:
+        x_ref_plan (T,12) / pf_plan (T,3) shared by the batch, or (B,T,12) /
+        (B,T,3) one per robot.  C is (N,) shared or (B,N)."""
+        import torch
+        N = self.N
+        B = x_in.shape[0]
+        shared = x_ref_plan.dim() == 2
+        T = x_ref_plan.shape[-2]
+        for t_, last in ((x_ref_plan, 12), (pf_plan, 3)):
+            if t_.dtype != torch.float64 or not t_.is_cuda or not t_.is_contiguous() \
+                    or t_.shape[-1] != last or t_.shape[-2] != T or (t_.dim() == 2) != shared:
+                raise ValueError('plans must be contiguous float64 cuda tensors (T,12)/(T,3) '
+                                 'or (B,T,12)/(B,T,3)')
+        if not shared and x_ref_plan.shape[0] != B:
+            raise ValueError('per-robot plans need a leading batch dimension B')
+        C_bs = 0 if C.dim() == 1 else N
+        if out is None:
+            dev = x_in.device
+            out = dict(u=torch.empty((B, N, 6), dtype=torch.float64, device=dev),
+                       obj=torch.empty(B, dtype=torch.float64, device=dev),
+                       status=torch.empty(B, dtype=torch.int32, device=dev),
+                       iters=torch.empty(B, dtype=torch.int32, device=dev))
+        s = stream if stream is not None else torch.cuda.current_stream(x_in.device).cuda_stream
+        rc = self._lib.hmpc_mpcontrol_plan_batch(
+            self._h, B, 1 if init else 0, _ptr(x_in), _ptr(x_ref_plan), _ptr(pf_plan), T,
+            0 if shared else T, int(k), int(mpc_factor), _ptr(C), C_bs, _ptr(mu), _ptr(x_prev),
+            _ptr(out['u']), _ptr(out.get('obj')), _ptr(out['status']), _ptr(out.get('iters')),
+            ctypes.c_void_p(s))
+        self._check(rc, 'hmpc_mpcontrol_plan_batch')
+        return out
+
+    def plant_device(self, X, U, U_bstride, pf, pf_bstride, pf_sstride, n_steps, dt, J,
+                     X_hist=None, x_out=None, stream=None):
+        """n_steps RK4 plant steps (src/robotrunner.py:126-164) on X (B,13)
+        in place; see hmpc_plant_batch for the strides."""
+        import torch
+        B = X.shape[0]
+        if tuple(X.shape) != (B, 13) or X.dtype != torch.float64 or not X.is_cuda \
+                or not X.is_contiguous():
+            raise ValueError('X must be a contiguous float64 cuda tensor (B,13)')
+        Jh = np.ascontiguousarray(np.asarray(J, dtype=np.float64).reshape(9))
+        s = stream if stream is not None else torch.cuda.current_stream(X.device).cuda_stream
+        rc = self._lib.hmpc_plant_batch(self._h, B, int(n_steps), float(dt), Jh.ctypes.data_as(_D),
+                                        _ptr(X), _ptr(U), int(U_bstride), _ptr(pf), int(pf_bstride),
+                                        int(pf_sstride), _ptr(X_hist), _ptr(x_out),
+                                        ctypes.c_void_p(s))
+        self._check(rc, 'hmpc_plant_batch')
+
+    def convert_device(self, X, x, stream=None):
+        """x (B,12) = convert(X (B,13)) (src/robotrunner.py:19-28)."""
+        import torch
+        s = stream if stream is not None else torch.cuda.current_stream(X.device).cuda_stream
+        rc = self._lib.hmpc_convert_batch(self._h, X.shape[0], _ptr(X), _ptr(x), ctypes.c_void_p(s))
+        self._check(rc, 'hmpc_convert_batch')
 
     def time_solve_device(self, x_in, x_lin, x_ref, pf, C, mu, out, reps, stream):
         """Mean kernel time (ms) over `reps` back-to-back launches, measured

@@ -16,6 +16,14 @@
  *                           (3f :41-69): builds the linearisation x_hat
  *                           (init: [x_in; x_ref], else the time shift of the
  *                           previous x*) on device, runs 1 or 2 solves
+ *   hmpc_mpcontrol_plan_batch <- the Runner's call (src/robotrunner.py:98-107):
+ *                           Mpc.mpcontrol on path_plan_grab(x_ref, k) /
+ *                           path_plan_grab(pf_ref, k) read in place from a
+ *                           device-resident plan (:228-230), no staging
+ *   hmpc_plant_batch     <- Runner.rk4_normalized / dynamics_ct
+ *                           (src/robotrunner.py:126-164) for n_steps
+ *                           low-level steps, then convert (:19-28)
+ *   hmpc_convert_batch   <- convert(X) (src/robotrunner.py:19-28)
  *   hmpc_destroy         <- object lifetime
  *
  * Conventions: every array is row-major, contiguous, float64, batch-major
@@ -111,6 +119,39 @@ int hmpc_mpcontrol_batch(hmpc_ctx* ctx, int64_t B, int init,
                          const double* C, const double* mu,
                          double* x_prev, double* u, double* obj, int32_t* status,
                          int32_t* iters, void* stream);
+
+/* Mpc.mpcontrol for B robots against a plan resident on the device
+   (src/robotrunner.py:98-107).  x_ref_plan [T,12] and pf_plan [T,3] are the
+   Runner's path_plan_init output (one per robot when plan_bstride = T rows,
+   shared when 0); robot b's window is rows k, k + f, ..., k + (N-1) f
+   (path_plan_grab, f = mpc_factor), which must lie inside [0, T).  C [N] is
+   gait_map(N, mpc_dt, t, t0), shared by the batch when C_bstride = 0.
+   Otherwise as hmpc_mpcontrol_batch.  Asynchronous. */
+int hmpc_mpcontrol_plan_batch(hmpc_ctx* ctx, int64_t B, int init,
+                              const double* x_in, const double* x_ref_plan,
+                              const double* pf_plan, int64_t T, int64_t plan_bstride,
+                              int64_t k, int mpc_factor,
+                              const double* C, int64_t C_bstride, const double* mu,
+                              double* x_prev, double* u, double* obj, int32_t* status,
+                              int32_t* iters, void* stream);
+
+/* The Runner's plant between two MPC solves, for B robots on the device:
+   n_steps RK4 steps of dynamics_ct with step dt and the input held
+   (src/robotrunner.py:104-113,126-164).  X [B,13] (p, q = [w,x,y,z], v, w:
+   the simulator's SE(3) state) is advanced in place.  The held input of robot
+   b is U[b*U_bstride .. +6) (pass the mpcontrol output u with U_bstride = 6N
+   to take its first row, as the Runner does).  Step s uses the foot position
+   pf[b*pf_bstride + s*pf_sstride .. +3) (the Runner's pf_ref[k + s]).
+   J [9] is the body inertia (host pointer); m, g, rh and J^-1 come from the
+   context.  X_hist [B,n_steps,13] (optional) receives every step's state,
+   x_out [B,12] (optional) convert(X) after the last one.  Asynchronous. */
+int hmpc_plant_batch(hmpc_ctx* ctx, int64_t B, int n_steps, double dt, const double* J,
+                     double* X, const double* U, int64_t U_bstride,
+                     const double* pf, int64_t pf_bstride, int64_t pf_sstride,
+                     double* X_hist, double* x_out, void* stream);
+
+/* x [B,12] = convert(X [B,13]) (src/robotrunner.py:19-28).  Asynchronous. */
+int hmpc_convert_batch(hmpc_ctx* ctx, int64_t B, const double* X, double* x, void* stream);
 
 /* Last HIP error string of this context ("" if none). */
 const char* hmpc_last_error(hmpc_ctx* ctx);
