@@ -45,6 +45,7 @@
 #include <utility>
 
 #include "hmpc_internal.h"
+#include "hmpc_model.h"
 
 namespace hmpc {
 
@@ -129,49 +130,6 @@ __device__ __forceinline__ void lds_wait(dbl2& a, dbl2& b) {
 template <int CNT>
 __device__ __forceinline__ void lds_wait(double& a) {
   asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(a) : "i"(CNT));
-}
-
-// ----------------------------------------------------------------------------
-// constants of Mpc.__init__ / build_qp (src/mpc_cvx_euler_3f.py:20,35,37,113-129)
-// ----------------------------------------------------------------------------
-constexpr double kQ[12] = {50, 50, 2, 1, 1, 50, 1, 1, 1, 10, 10, 10};   // :35
-constexpr double kRdiag = 0.001;   // R = 0.001 I   (:37)
-constexpr double kTermQ = 100.0;   // kf at k = N-1 (:113)
-constexpr double kFzMax = 206.0;   // f_max[2]      (:20)
-constexpr double kZmin = 0.1;      //               (:129)
-constexpr double kTol = 1e-10;     // scaled primal feasibility tolerance
-__device__ __forceinline__ double tau_lim(int c) { return c == 5 ? 4.0 : 7.78; }   // :123-128
-
-constexpr int ST_SOLVED = 0, ST_MAXIT = 1, ST_INFEAS = 2, ST_NUMERICAL = 3;
-
-// ----------------------------------------------------------------------------
-// cross-lane helpers (wave64; W waves per workgroup)
-// ----------------------------------------------------------------------------
-__device__ __forceinline__ double rdlane(double x, int l) {
-  long long b = __double_as_longlong(x);
-  int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffLL), l);
-  int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
-  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
-}
-__device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
-
-__device__ __forceinline__ double wave_sum(double x) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
-  return x;
-}
-
-__device__ __forceinline__ void argmin_combine(double& v, int& i, double v2, int i2) {
-  if (v2 < v || (v2 == v && i2 < i)) { v = v2; i = i2; }
-}
-
-__device__ __forceinline__ void wave_argmin(double& v, int& i) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    double v2 = __shfl_xor(v, o, 64);
-    int i2 = __shfl_xor(i, o, 64);
-    argmin_combine(v, i, v2, i2);
-  }
 }
 
 template <int W>
@@ -264,8 +222,9 @@ struct Lay {
   static constexpr int XS = ZB + e2(N + 1);        // [NT] primal broadcast
   static constexpr int RED = XS + NT;              // [4] cross-wave reductions (W <= 2)
   static constexpr int ZR = RED + 4;               // [2] a 0.0 for masked lanes' loads
+  static constexpr int XRV = ZR + 2;               // [2] x_ref view for phase 7: address, row stride
   // active-set state (phase 6); the Cholesky's column buffers overlay it
-  static constexpr int G0 = ZR + 2;
+  static constexpr int G0 = XRV + 2;
   static constexpr int UA = G0;                    // [QMAX] active multipliers
   static constexpr int ACT = UA + QMAX;            // [QMAX] active ids (int)
   static constexpr int CB = ACT + QMAX;            // [QMAX] c = Qw' w
@@ -295,104 +254,6 @@ struct Lay {
 };
 
 __device__ __forceinline__ int loff(int r) { return (r * (r + 1)) >> 1; }
-
-// S_t storage order (22 entries):
-//   0..8   per axis a: [pp, pv, vv] at 3a    (p_a = x[a], v_a = x[6+a])
-//   9..11  yaw: [tt, tw, ww]                 (theta_z = x[5], w_z = x[11])
-//   12..21 roll/pitch block y = (x3, x4, x9, x10):
-//          P00 P01 P11 M00 M01 M10 M11 Q00 Q01 Q11  (M_ij = S[x(3+i)][x(9+j)])
-// f = S e for the structured S (full 12 rows)
-__device__ __forceinline__ void s_times(const double* s, const double (&e)[12], double (&f)[12]) {
-#pragma unroll
-  for (int a = 0; a < 3; ++a) {
-    f[a] = s[3 * a] * e[a] + s[3 * a + 1] * e[6 + a];
-    f[6 + a] = s[3 * a + 1] * e[a] + s[3 * a + 2] * e[6 + a];
-  }
-  f[5] = s[9] * e[5] + s[10] * e[11];
-  f[11] = s[10] * e[5] + s[11] * e[11];
-  const double P00 = s[12], P01 = s[13], P11 = s[14], M00 = s[15], M01 = s[16], M10 = s[17],
-               M11 = s[18], Q00 = s[19], Q01 = s[20], Q11 = s[21];
-  f[3] = P00 * e[3] + P01 * e[4] + M00 * e[9] + M01 * e[10];
-  f[4] = P01 * e[3] + P11 * e[4] + M10 * e[9] + M11 * e[10];
-  f[9] = M00 * e[3] + M10 * e[4] + Q00 * e[9] + Q01 * e[10];
-  f[10] = M01 * e[3] + M11 * e[4] + Q01 * e[9] + Q11 * e[10];
-}
-
-// x <- Ad x with Ad = I + dt A(psi): p += dt v; theta += dt Rz(psi) w
-// (src/mpc_cvx_euler_3f.py:27,87,91; rz of src/utils.py:46-51)
-__device__ __forceinline__ void ad_times(double (&x)[12], double dt, double cp, double sp) {
-#pragma unroll
-  for (int a = 0; a < 3; ++a) x[a] = fma(dt, x[6 + a], x[a]);
-  const double w0 = x[9], w1 = x[10];
-  x[3] = x[3] + ((cp * dt) * w0 + (sp * dt) * w1);
-  x[4] = x[4] + ((-sp * dt) * w0 + (cp * dt) * w1);
-  x[5] = fma(dt, x[11], x[5]);
-}
-// g <- Ad' g
-__device__ __forceinline__ void adt_times(double (&g)[12], double dt, double cp, double sp) {
-#pragma unroll
-  for (int a = 0; a < 3; ++a) g[6 + a] = fma(dt, g[a], g[6 + a]);
-  const double g3 = g[3], g4 = g[4];
-  g[9] = g[9] + ((cp * dt) * g3 + (-sp * dt) * g4);
-  g[10] = g[10] + ((sp * dt) * g3 + (cp * dt) * g4);
-  g[11] = fma(dt, g[5], g[11]);
-}
-
-// The same two maps lane-parallel: lane r < 12 holds component r.  The
-// cross terms come from other lanes (readlane / bpermute); lanes >= 12 pass
-// their value through unchanged.
-__device__ __forceinline__ double ad_lane(double x, double dt, double cp, double sp) {
-  const int r = threadIdx.x;
-  const double xv = __shfl(x, (int)((threadIdx.x + 6) & 63), 64);   // x[r+6] for r < 3
-  const double w0 = rdlane(x, 9), w1 = rdlane(x, 10), w2 = rdlane(x, 11);
-  double d = 0.0;
-  d = (r < 3) ? xv : d;
-  d = (r == 3) ? (cp * w0 + sp * w1) : d;
-  d = (r == 4) ? (cp * w1 - sp * w0) : d;
-  d = (r == 5) ? w2 : d;
-  return fma(dt, d, x);
-}
-__device__ __forceinline__ double adt_lane(double g, double dt, double cp, double sp) {
-  const int r = threadIdx.x;
-  const double gv = __shfl(g, (int)((threadIdx.x + 58) & 63), 64);  // g[r-6] for 6 <= r < 9
-  const double g3 = rdlane(g, 3), g4 = rdlane(g, 4), g5 = rdlane(g, 5);
-  double d = 0.0;
-  d = (r >= 6 && r < 9) ? gv : d;
-  d = (r == 9) ? (cp * g3 - sp * g4) : d;
-  d = (r == 10) ? (sp * g3 + cp * g4) : d;
-  d = (r == 11) ? g5 : d;
-  return fma(dt, d, g);
-}
-__device__ __forceinline__ double qdiag(int r) {   // Q[r][r], 0 beyond the state
-  return (r == 0 || r == 1 || r == 5) ? 50.0 : (r == 2 ? 2.0 : (r >= 9 && r < 12) ? 10.0 : (r < 12 ? 1.0 : 0.0));
-}
-
-// rows 6..8 of Bd_k, column c2 (< 3): 3f dt/m I (:28), 2f Rz'(psi) dt/m (2f :87)
-template <int VAR>
-__device__ __forceinline__ double bv(int r, int c2, double dtm, double cp, double sp) {
-  if constexpr (VAR == 3) {
-    return r == c2 ? dtm : 0.0;
-  } else {
-    // Rz' = [[c, -s, 0], [s, c, 0], [0, 0, 1]]
-    if (r == 2 || c2 == 2) return (r == c2) ? dtm : 0.0;
-    if (r == c2) return cp * dtm;
-    return (r == 0) ? -sp * dtm : sp * dtm;
-  }
-}
-
-// 2 Bd_j[:, c2]' y[6..11]  (rows 0..5 of Bd are zero)
-template <int VAR>
-__device__ __forceinline__ double bd_dot(int c2, const double (&y)[12], const double* bw, double dtm,
-                                         double cp, double sp) {
-  double acc = 0.0;
-  if (c2 < 3) {
-#pragma unroll
-    for (int r = 0; r < 3; ++r) acc = fma(bv<VAR>(r, c2, dtm, cp, sp), y[6 + r], acc);
-  }
-#pragma unroll
-  for (int r = 0; r < 3; ++r) acc = fma(bw[6 * r + c2], y[9 + r], acc);
-  return 2.0 * acc;
-}
 
 // ----------------------------------------------------------------------------
 // triangular sweeps.  The factor is kept as the unit lower M = L diag(L)^-1:
@@ -551,6 +412,10 @@ solve_kernel(SolveArgs a) {
   // x_ref / pf / C may be strided views (a resident plan, path_plan_grab
   // src/robotrunner.py:228-230: rows k, k+f, ...; batch stride 0 = shared)
   const double* xrf = a.x_ref + b * a.xref_bs;
+  if (tid == 0) {   // kept in LDS, not in SGPRs, until phase 7 reads x_ref again
+    reinterpret_cast<const double**>(sm + L::XRV)[0] = xrf;
+    reinterpret_cast<int*>(sm + L::XRV + 1)[0] = a.xref_rs;
+  }
   for (int i = tid; i < 12; i += NT) sm[L::XIN + i] = a.x_in[b * 12 + i];
   for (int i = tid; i < 12 * N; i += NT) {
     const int r = i / 12, c = i - 12 * r;
@@ -578,6 +443,8 @@ solve_kernel(SolveArgs a) {
   HMPC_STAMP(1);
 
   // ---------------- phase 1: gen_dt_dynamics (lane k < N) -------------------
+  // (hmpc_model.h's stage_dynamics() inline: the call form costs 8 B/lane
+  // more scratch in this kernel)
   if (tid < N) {
     const int k = tid;
     const double psi = sm[L::XLIN + 12 * k + 5];
@@ -1234,7 +1101,8 @@ solve_kernel(SolveArgs a) {
     double xr = tid < 12 ? sm[L::XIN + tid] : 0.0;
     if (tid < 12) xo[tid] = xr;
     const double qr = qdiag(tid_o);   // (not CSE-d with phase 2's copy)
-    const double* xrf = a.x_ref + b * a.xref_bs;
+    const double* xrf = reinterpret_cast<const double* const*>(sm + L::XRV)[0];
+    const int xrs = reinterpret_cast<const int*>(sm + L::XRV + 1)[0];
     const int rw = (tid >= 9 && tid < 12) ? tid - 9 : 0;   // my row of Bd's omega block
     const int rv = (tid >= 6 && tid < 9) ? tid - 6 : 0;    // my row of Bd's velocity block
     double objl = 0.0;
@@ -1256,7 +1124,7 @@ solve_kernel(SolveArgs a) {
       const double bu = (tid >= 9 && tid < 12) ? bw_u : ((tid >= 6 && tid < 9) ? bv_u : 0.0);
       xr = ad_lane(xr, dt, cp, sp) + bu + ((tid == 8) ? -a.g * dt : 0.0);
       const double kf = (k == N - 1) ? kTermQ : 1.0;
-      const double e = xr - (tid < 12 ? xrf[k * a.xref_rs + tid] : 0.0);
+      const double e = xr - (tid < 12 ? xrf[k * xrs + tid] : 0.0);
       objl = fma(kf * qr * e, e, objl);
       if (k < N - 1 && tid < 6) {
         const double ub = a.uref_aliased ? ((sm[L::CC + N - 1] != 0.0) ? 2.0 * a.m * a.g : 0.0)
