@@ -29,6 +29,9 @@ struct hmpc_ctx {
   size_t dbuf_bytes = 0;
   int32_t* scratch_i32 = nullptr;
   int64_t scratch_n = 0;
+  // generic-horizon kernel workspace (hmpc_wide.hip)
+  double* wsbuf = nullptr;
+  int wsgroups = 0;
   hipStream_t own_stream = nullptr;
 };
 
@@ -62,7 +65,38 @@ hmpc::SolveArgs make_args(hmpc_ctx* c, int64_t B, const double* x_in, const doub
   a.xref_bs = 12 * (int64_t)N; a.xref_rs = 12;
   a.pf_bs = 3 * (int64_t)N; a.pf_rs = 3;
   a.C_bs = N;
+  a.ws = nullptr; a.ws_stride = 0; a.ws_groups = 0;
   return a;
+}
+
+// Horizons without a dedicated kernel: make sure the context's workspace
+// covers min(B, kMaxGroups) resident workgroups and point the args at it.
+constexpr int kMaxGroups = 512;
+constexpr size_t kWsBudget = (size_t)4 << 30;   // bytes
+
+int prepare_ws(hmpc_ctx* c, int64_t B, hmpc::SolveArgs& a) {
+  if (hmpc::horizon_compiled(c->variant, c->N)) return HMPC_OK;
+  const hmpc::WideLayout Lw(c->N);
+  const size_t per = (size_t)Lw.total * sizeof(double);
+  int64_t want = B < kMaxGroups ? B : kMaxGroups;
+  const int64_t cap = (int64_t)(kWsBudget / per) > 0 ? (int64_t)(kWsBudget / per) : 1;
+  if (want > cap) want = cap;
+  if (want < 1) want = 1;
+  if (want > c->wsgroups) {
+    if (c->wsbuf) (void)hipFree(c->wsbuf);
+    c->wsbuf = nullptr;
+    c->wsgroups = 0;
+    hipError_t e = hipMalloc(&c->wsbuf, per * (size_t)want);
+    if (e != hipSuccess) {
+      c->err = std::string("workspace hipMalloc: ") + hipGetErrorString(e);
+      return HMPC_ERR_NOMEM;
+    }
+    c->wsgroups = (int)want;
+  }
+  a.ws = c->wsbuf;
+  a.ws_stride = Lw.total;
+  a.ws_groups = c->wsgroups;
+  return HMPC_OK;
 }
 
 __global__ void combine_status(int64_t B, const int32_t* s1, const int32_t* i1, int32_t* s2,
@@ -123,6 +157,7 @@ int hmpc_destroy(hmpc_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->dbuf) (void)hipFree(c->dbuf);
   if (c->scratch_i32) (void)hipFree(c->scratch_i32);
+  if (c->wsbuf) (void)hipFree(c->wsbuf);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   delete c;
   return HMPC_OK;
@@ -138,6 +173,8 @@ int hmpc_solve_batch(hmpc_ctx* c, int64_t B, const double* x_in, const double* x
   if (rc != HMPC_OK || B == 0) return rc;
   HMPC_HIP(c, hipSetDevice(c->device));
   hmpc::SolveArgs a = make_args(c, B, x_in, x_lin, x_ref, pf, C, mu, u, x, obj, status, iters, 0);
+  rc = prepare_ws(c, B, a);
+  if (rc != HMPC_OK) return rc;
   if (!hmpc::launch_solve(c->variant, c->N, a, (hipStream_t)stream)) return HMPC_ERR_UNSUPPORTED;
   HMPC_HIP(c, hipGetLastError());
   return HMPC_OK;
@@ -156,6 +193,8 @@ int hmpc_time_solve_batch(hmpc_ctx* c, int64_t B, const double* x_in, const doub
   HMPC_HIP(c, hipEventCreate(&e0));
   HMPC_HIP(c, hipEventCreate(&e1));
   hmpc::SolveArgs a = make_args(c, B, x_in, x_lin, x_ref, pf, C, mu, u, x, obj, status, iters, 0);
+  rc = prepare_ws(c, B, a);
+  if (rc != HMPC_OK) return rc;
   HMPC_HIP(c, hipEventRecord(e0, s));
   for (int r = 0; r < reps; ++r) hmpc::launch_solve(c->variant, c->N, a, s);
   HMPC_HIP(c, hipEventRecord(e1, s));
@@ -209,6 +248,8 @@ int hmpc_solve_batch_host(hmpc_ctx* c, int64_t B, const double* x_in, const doub
   if (mu) HMPC_HIP(c, hipMemcpyAsync(d_mu, mu, 8 * B, hipMemcpyHostToDevice, s));
   hmpc::SolveArgs a = make_args(c, B, d_xin, d_xlin, d_xref, d_pf, d_C, mu ? d_mu : nullptr,
                                 d_u, d_x, d_obj, d_st, d_it, 0);
+  rc = prepare_ws(c, B, a);
+  if (rc != HMPC_OK) return rc;
   if (!hmpc::launch_solve(c->variant, c->N, a, s)) return HMPC_ERR_UNSUPPORTED;
   HMPC_HIP(c, hipGetLastError());
   HMPC_HIP(c, hipMemcpyAsync(u, d_u, 8 * B * 6 * N, hipMemcpyDeviceToHost, s));
@@ -230,6 +271,12 @@ int mpcontrol_impl(hmpc_ctx* c, int64_t B, int init, const double* x_in, const d
                    const hmpc::SolveArgs* view) {
   HMPC_HIP(c, hipSetDevice(c->device));
   hipStream_t s = (hipStream_t)stream;
+  {
+    hmpc::SolveArgs probe = make_args(c, B, x_in, x_prev, x_ref, pf, C, mu, u, x_prev, obj, status,
+                                      iters, 0);
+    const int rc = prepare_ws(c, B, probe);
+    if (rc != HMPC_OK) return rc;
+  }
   auto args = [&](int32_t* st, int32_t* it, double* ob, int mode) {
     hmpc::SolveArgs a = make_args(c, B, x_in, x_prev, x_ref, pf, C, mu, u, x_prev, ob, st, it, mode);
     if (view) {
@@ -237,6 +284,7 @@ int mpcontrol_impl(hmpc_ctx* c, int64_t B, int init, const double* x_in, const d
       a.pf_bs = view->pf_bs; a.pf_rs = view->pf_rs;
       a.C_bs = view->C_bs;
     }
+    (void)prepare_ws(c, B, a);   // allocated above: only sets the pointers
     return a;
   };
   if (init) {

@@ -18,16 +18,21 @@ bool launch_solve(int variant, int N, const SolveArgs& a, hipStream_t s) {
   if (N == n) return launch_solve_n##n(variant, a, s);
   HMPC_HORIZON_LIST(HMPC_CASE)
 #undef HMPC_CASE
-  return false;
+  return launch_solve_wide(variant, N, a, s);
 }
 
-bool horizon_supported(int variant, int N) {
+bool horizon_compiled(int variant, int N) {
   if (variant != 2 && variant != 3) return false;
 #define HMPC_CASE(n) \
   if (N == n) return true;
   HMPC_HORIZON_LIST(HMPC_CASE)
 #undef HMPC_CASE
   return false;
+}
+
+bool horizon_supported(int variant, int N) {
+  if (variant != 2 && variant != 3) return false;
+  return horizon_compiled(variant, N) || (N >= 1 && N <= kWideNmax);
 }
 
 int supported_horizons(int variant, int* Ns, int cap) {

@@ -34,6 +34,54 @@ struct SolveArgs {
   // / N); a batch stride of 0 shares one plan window across the batch
   int64_t xref_bs, pf_bs, C_bs;
   int xref_rs, pf_rs;
+  // global workspace of the generic-horizon kernel (hmpc_wide.hip): one
+  // WideLayout(N).total block per resident workgroup
+  double* ws;
+  int64_t ws_stride;
+  int ws_groups;
+};
+
+// Horizons without a dedicated kernel run on the generic kernel up to this N.
+constexpr int kWideNmax = 128;
+
+// Per-instance workspace of the generic-horizon kernel, in doubles.  The
+// three NV x NV blocks (H -> L, J = L^-T Q, R) dominate: 3 MB at N = 60.
+struct WideLayout {
+  int64_t XIN, CC, CS, BW, ZB, XL, XR, PF, SS, DG, AJ;         // per stage
+  int64_t HV, XV, DV, ZV, WV, UO, RV, UA, FR, POS, ACT, ISA;   // per variable
+  int64_t RM, H, J, total;
+  __host__ __device__ explicit WideLayout(int N) {
+    const int64_t NV = 6 * (int64_t)N;
+    auto up = [](int64_t x) { return (x + 15) & ~(int64_t)15; };   // 128-B aligned
+    int64_t o = 0;
+    XIN = o; o = up(o + 12);
+    CC = o; o = up(o + N);
+    CS = o; o = up(o + 2 * N);
+    BW = o; o = up(o + 18 * N);
+    ZB = o; o = up(o + N + 1);
+    XL = o; o = up(o + 12 * N);
+    XR = o; o = up(o + 12 * N);
+    PF = o; o = up(o + 3 * N);
+    SS = o; o = up(o + 22 * N);
+    DG = o; o = up(o + 12 * N);
+    AJ = o; o = up(o + 6 * N);
+    HV = o; o = up(o + NV);
+    XV = o; o = up(o + NV);
+    DV = o; o = up(o + NV);
+    ZV = o; o = up(o + NV);
+    WV = o; o = up(o + NV);
+    UO = o; o = up(o + NV);
+    RV = o; o = up(o + NV);
+    UA = o; o = up(o + NV + 1);
+    FR = o; o = up(o + NV);          // int slots (one per double)
+    POS = o; o = up(o + NV);
+    ACT = o; o = up(o + NV + 1);
+    ISA = o; o = up(o + 4 * NV);
+    RM = o; o = up(o + NV * NV);
+    H = o; o = up(o + NV * NV);
+    J = o; o = up(o + NV * NV);
+    total = o;
+  }
 };
 
 // The Runner's plant (hmpc_plant.hip): n_steps RK4 steps of dynamics_ct with
@@ -57,7 +105,10 @@ void launch_convert(int64_t B, const double* X, double* x, hipStream_t s);
 // Launch the solve kernel for (variant, N).  Returns false when no kernel
 // is compiled for that combination.
 bool launch_solve(int variant, int N, const SolveArgs& a, hipStream_t stream);
-bool horizon_supported(int variant, int N);
+// the generic-horizon kernel (any 1 <= N <= kWideNmax); a.ws must be set
+bool launch_solve_wide(int variant, int N, const SolveArgs& a, hipStream_t stream);
+bool horizon_supported(int variant, int N);   // compiled, or generic (N <= kWideNmax)
+bool horizon_compiled(int variant, int N);    // a dedicated one-wavefront kernel
 int supported_horizons(int variant, int* Ns, int cap);
 
 }  // namespace hmpc

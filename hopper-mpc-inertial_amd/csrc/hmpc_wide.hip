@@ -1,0 +1,620 @@
+// hmpc_wide.hip -- the same QP for horizons without a dedicated kernel
+// (the Runner's default N = 60, src/robotrunner.py:46, and any other
+// 1 <= N <= kWideNmax).
+//
+// The one-wavefront kernel (hmpc_kernels.hip) keeps a row of the condensed
+// Hessian in registers and the whole factor in LDS; at N = 60 the factor
+// alone is 520 KB.  Here one 256-thread workgroup solves an instance out of a
+// per-workgroup global workspace (WideLayout, L2-resident), fixed variables
+// are compacted away first (swing forces, 2f fy: NF <= NV free variables),
+// and the dual active set is the classic Goldfarb-Idnani form with an
+// explicit J = L^-T Q, whose every step is a parallel sweep over J:
+//
+//   0  inputs -> workspace (plan views as in the fast kernel)
+//   1  gen_dt_dynamics per stage (3f :71-94, 2f :70-94)
+//   2  free response, cost-to-go S_t, adjoint (wave 0; same recursions as the
+//      fast kernel's phase 2)
+//   3  free-variable map; Hessian rows over the free variables (thread per
+//      row: g_j = Ad_{j+1}' g_{j+1} from S_{i+1} B_i e_c) and gradient
+//   4  Cholesky H = L L' (right-looking, trailing rows updated coalesced)
+//   5  J = L^-T (thread per column of L^-1, independent forward substitutions)
+//   6  Goldfarb-Idnani: d = J' n_p from the <= N nonzeros of n_p (rows of
+//      J), z = J2 d2 (wave-per-row dot products), adds by ONE Householder
+//      reflection of J's trailing columns (two parallel passes; Givens would
+//      be NF - q dependent rotations), drops by Givens on R and J
+//   7  outputs as the fast kernel (x* rollout, objective)
+//
+// Constraints and tolerances are those of the fast kernel (one id per
+// variable and slot: torque box :123-128, fz box + friction :141-146,
+// z >= 0.1 :129).
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "hmpc_internal.h"
+#include "hmpc_model.h"
+
+namespace hmpc {
+
+namespace {
+
+constexpr int WT = 256;               // threads per workgroup
+constexpr int WW = WT / 64;           // waves
+constexpr int NVMAX = 6 * kWideNmax;  // LDS vectors
+
+struct Shared {
+  double red[WW];
+  int ired[WW];
+  double vec[NVMAX];   // a broadcast vector (Cholesky column, d, Householder v)
+  double vec2[NVMAX];
+  double npv[kWideNmax + 2];   // n_p: <= N nonzeros (z rows), else <= 2
+  int npi[kWideNmax + 2];
+  int npn;
+  int nf;
+  int p;
+  int kd;
+  int flag;
+  double best, bp, t1, sp, gc, gs;
+};
+
+__device__ double block_sum(double x, Shared& sh) {
+  x = wave_sum(x);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) sh.red[threadIdx.x >> 6] = x;
+  __syncthreads();
+  double s = 0.0;
+#pragma unroll
+  for (int w = 0; w < WW; ++w) s += sh.red[w];
+  return s;
+}
+
+__device__ void block_argmin(double& v, int& i, Shared& sh) {
+  wave_argmin(v, i);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) {
+    sh.red[threadIdx.x >> 6] = v;
+    sh.ired[threadIdx.x >> 6] = i;
+  }
+  __syncthreads();
+  v = sh.red[0];
+  i = sh.ired[0];
+#pragma unroll
+  for (int w = 1; w < WW; ++w) argmin_combine(v, i, sh.red[w], sh.ired[w]);
+}
+
+// out[i] = sum_{k in [k0, n)} M[i*ld + k] vec[k] for rows i < n: one wave per
+// row, lanes over k (coalesced), then a wave reduction.
+__device__ void rows_dot(const double* M, int ld, int n, int k0, const double* vec, double* out) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int i = w; i < n; i += WW) {
+    const double* row = M + (int64_t)i * ld;
+    double acc = 0.0;
+    for (int k = k0 + lane; k < n; k += 64) acc = fma(row[k], vec[k], acc);
+    acc = wave_sum(acc);
+    if (lane == 0) out[i] = acc;
+  }
+}
+
+__device__ __forceinline__ void gfence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup"); }
+
+template <int VAR>
+__device__ void wide_solve(const SolveArgs& a, const int N, const int64_t b, double* ws, Shared& sh) {
+  const WideLayout Lw(N);
+  const int tid = threadIdx.x;
+  const int NV = 6 * N;
+  const double dt = a.dt, dtm = dt / a.m;
+  double* xin = ws + Lw.XIN;
+  double* cc = ws + Lw.CC;
+  double* cs = ws + Lw.CS;
+  double* bw = ws + Lw.BW;
+  double* zb = ws + Lw.ZB;
+  double* xl = ws + Lw.XL;
+  double* xr = ws + Lw.XR;
+  double* pf = ws + Lw.PF;
+  double* ss = ws + Lw.SS;
+  double* dg = ws + Lw.DG;
+  double* aj = ws + Lw.AJ;
+  double* hv = ws + Lw.HV;
+  double* xv = ws + Lw.XV;
+  double* dv = ws + Lw.DV;
+  double* zv = ws + Lw.ZV;
+  double* wv = ws + Lw.WV;
+  double* uo = ws + Lw.UO;
+  double* rv = ws + Lw.RV;
+  double* ua = ws + Lw.UA;
+  int* fr = reinterpret_cast<int*>(ws + Lw.FR);
+  int* pos = reinterpret_cast<int*>(ws + Lw.POS);
+  int* act = reinterpret_cast<int*>(ws + Lw.ACT);
+  int* isa = reinterpret_cast<int*>(ws + Lw.ISA);
+  double* Rm = ws + Lw.RM;
+  double* H = ws + Lw.H;
+  double* J = ws + Lw.J;
+  const int ld = NV;   // row stride of H, J, R
+
+  // ---------------- 0: inputs ------------------------------------------------
+  {
+    const double* xrf = a.x_ref + b * a.xref_bs;
+    for (int i = tid; i < 12; i += WT) xin[i] = a.x_in[b * 12 + i];
+    for (int i = tid; i < 12 * N; i += WT) xr[i] = xrf[(int64_t)(i / 12) * a.xref_rs + i % 12];
+    for (int i = tid; i < 3 * N; i += WT) pf[i] = a.pf[b * a.pf_bs + (int64_t)(i / 3) * a.pf_rs + i % 3];
+    for (int i = tid; i < N; i += WT) cc[i] = a.C[b * a.C_bs + i];
+    gfence();
+    __syncthreads();
+    const double* xp = a.x_lin + b * 12 * (N + 1);
+    for (int i = tid; i < 12 * N; i += WT) {
+      const int r = i / 12, c = i - 12 * r;
+      double v;
+      if (a.shift_mode == 0) v = xp[i];
+      else if (a.shift_mode == 1) v = r == 0 ? xin[c] : xr[i - 12];   // [x_in; x_ref] (3f :52-53)
+      else v = r == 0 ? xin[c] : xp[(r + 1) * 12 + c];               // time shift (3f :59-62)
+      xl[i] = v;
+    }
+    gfence();
+    __syncthreads();
+  }
+  // ---------------- 1: gen_dt_dynamics --------------------------------------
+  for (int k = tid; k < N; k += WT) stage_dynamics<VAR>(k, xl, pf, a.Jinv, a.rh, dt, cs, bw);
+  gfence();
+  __syncthreads();
+  // ---------------- 2: free response, S_t, adjoint (wave 0) -----------------
+  if (tid < 64) {
+    double xrr = tid < 12 ? xin[tid] : 0.0;
+    const double qr = qdiag(tid);
+    double s[22];
+#pragma unroll
+    for (int a3 = 0; a3 < 3; ++a3) {
+      s[3 * a3] = kTermQ * kQ[a3];
+      s[3 * a3 + 1] = 0.0;
+      s[3 * a3 + 2] = kTermQ * kQ[6 + a3];
+    }
+    s[9] = kTermQ * kQ[5]; s[10] = 0.0; s[11] = kTermQ * kQ[11];
+    s[12] = kTermQ * kQ[3]; s[13] = 0.0; s[14] = kTermQ * kQ[4];
+    s[15] = s[16] = s[17] = s[18] = 0.0;
+    s[19] = kTermQ * kQ[9]; s[20] = 0.0; s[21] = kTermQ * kQ[10];
+    if (tid == 2) zb[0] = xrr;
+    if (tid == 0)
+      for (int e = 0; e < 22; ++e) ss[22 * (N - 1) + e] = s[e];
+    for (int k = 0; k < N; ++k) {
+      const double cp = cs[2 * k], sp = cs[2 * k + 1];
+      xrr = ad_lane(xrr, dt, cp, sp) + ((tid == 8) ? -a.g * dt : 0.0);
+      const double kf = (k == N - 1) ? kTermQ : 1.0;
+      if (tid < 12) dg[12 * k + tid] = kf * qr * (xrr - xr[12 * k + tid]);
+      if (tid == 2) zb[k + 1] = xrr;
+      const int t = N - 1 - k;
+      if (t >= 1) {
+        const double ct = cs[2 * t], st = cs[2 * t + 1];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int o = 3 * q;
+          const double aa = s[o], bb = s[o + 1], cc2 = s[o + 2];
+          s[o + 1] = fma(dt, aa, bb);
+          s[o + 2] = cc2 + dt * (2.0 * bb + dt * aa);
+        }
+        const double D00 = ct * dt, D01 = st * dt, D10 = -st * dt, D11 = ct * dt;
+        const double P00 = s[12], P01 = s[13], P11 = s[14];
+        const double M00 = s[15], M01 = s[16], M10 = s[17], M11 = s[18];
+        const double N00 = M00 + (P00 * D00 + P01 * D10), N01 = M01 + (P00 * D01 + P01 * D11);
+        const double N10 = M10 + (P01 * D00 + P11 * D10), N11 = M11 + (P01 * D01 + P11 * D11);
+        const double A00 = D00 * N00 + D10 * N10, A01 = D00 * N01 + D10 * N11;
+        const double A11 = D01 * N01 + D11 * N11;
+        const double B00 = M00 * D00 + M10 * D10, B01 = M00 * D01 + M10 * D11;
+        const double B11 = M01 * D01 + M11 * D11;
+        s[19] += A00 + B00;
+        s[20] += A01 + B01;
+        s[21] += A11 + B11;
+        s[15] = N00; s[16] = N01; s[17] = N10; s[18] = N11;
+#pragma unroll
+        for (int a3 = 0; a3 < 3; ++a3) {
+          s[3 * a3] += kQ[a3];
+          s[3 * a3 + 2] += kQ[6 + a3];
+        }
+        s[9] += kQ[5]; s[11] += kQ[11];
+        s[12] += kQ[3]; s[14] += kQ[4];
+        s[19] += kQ[9]; s[21] += kQ[10];
+        if (tid == 0)
+          for (int e = 0; e < 22; ++e) ss[22 * (t - 1) + e] = s[e];
+      }
+    }
+    gfence();
+    double ar = tid < 12 ? dg[12 * (N - 1) + tid] : 0.0;
+    if (tid >= 6 && tid < 12) aj[6 * (N - 1) + tid - 6] = ar;
+    for (int t = N - 1; t >= 1; --t) {
+      ar = adt_lane(ar, dt, cs[2 * t], cs[2 * t + 1]) + (tid < 12 ? dg[12 * (t - 1) + tid] : 0.0);
+      if (tid >= 6 && tid < 12) aj[6 * (t - 1) + tid - 6] = ar;
+    }
+  }
+  // ---------------- 3: free variables, Hessian rows, gradient ----------------
+  if (tid == 0) {
+    int nf = 0;
+    for (int v = 0; v < NV; ++v) {
+      const int k = v / 6, c = v - 6 * k;
+      const bool fixed = (c < 3 && cc[k] == 0.0) || (VAR == 2 && c == 1);   // :134-136, 2f :129
+      pos[v] = fixed ? -1 : nf;
+      if (!fixed) fr[nf++] = v;
+    }
+    sh.nf = nf;
+  }
+  gfence();
+  __syncthreads();
+  const int NF = sh.nf;
+  const double ubar_alias = (cc[N - 1] != 0.0) ? 2.0 * a.m * a.g : 0.0;
+  for (int r = tid; r < NF; r += WT) {
+    const int v = fr[r];
+    const int ii = v / 6, ci = v - 6 * ii;
+    const double cpi = cs[2 * ii], spi = cs[2 * ii + 1];
+    const double* bwi = bw + 18 * ii;
+    double e0[12], f[12], g[12];
+    for (int q = 0; q < 6; ++q) e0[q] = 0.0;
+    for (int q = 0; q < 3; ++q) e0[6 + q] = ci < 3 ? bv<VAR>(q, ci, dtm, cpi, spi) : 0.0;
+    for (int q = 0; q < 3; ++q) e0[9 + q] = bwi[6 * q + ci];
+    s_times(ss + 22 * ii, e0, f);
+    double* Hr = H + (int64_t)r * ld;
+    for (int c2 = 0; c2 <= ci; ++c2) {   // diagonal block, columns <= mine
+      const int pw = pos[6 * ii + c2];
+      if (pw < 0) continue;
+      double hd = bd_dot<VAR>(c2, f, bwi, dtm, cpi, spi);
+      if (c2 == ci && ii != N - 1) hd += 2.0 * kRdiag;
+      Hr[pw] = hd;
+    }
+    double hacc = 0.0;
+    for (int q = 0; q < 6; ++q) hacc = fma(e0[6 + q], aj[6 * ii + q], hacc);
+    for (int q = 0; q < 12; ++q) g[q] = f[q];
+    for (int j = ii - 1; j >= 0; --j) {
+      adt_times(g, dt, cs[2 * (j + 1)], cs[2 * (j + 1) + 1]);
+      const double cp = cs[2 * j], sp = cs[2 * j + 1];
+      for (int c2 = 0; c2 < 6; ++c2) {
+        const int pw = pos[6 * j + c2];
+        if (pw >= 0) Hr[pw] = bd_dot<VAR>(c2, g, bw + 18 * j, dtm, cp, sp);
+      }
+    }
+    double ub = 0.0;
+    if (ci == 2) ub = a.uref_aliased ? ubar_alias : ((cc[ii] != 0.0) ? 2.0 * a.m * a.g : 0.0);
+    const double Vj = (ii == N - 1) ? 0.0 : kRdiag;
+    hv[r] = 2.0 * hacc - 2.0 * Vj * ub;
+  }
+  gfence();
+  __syncthreads();
+
+  int status = ST_SOLVED;
+  // ---------------- 4: Cholesky --------------------------------------------
+  for (int k = 0; k < NF; ++k) {
+    const double piv = H[(int64_t)k * ld + k];
+    if (!(piv > 0.0)) { status = ST_NUMERICAL; break; }
+    const double lkk = sqrt(piv), rl = 1.0 / lkk;
+    for (int i = k + 1 + tid; i < NF; i += WT) {
+      const double l = H[(int64_t)i * ld + k] * rl;
+      H[(int64_t)i * ld + k] = l;
+      sh.vec[i] = l;
+    }
+    gfence();
+    __syncthreads();   // every thread has read the pivot; column k published
+    if (tid == 0) H[(int64_t)k * ld + k] = lkk;
+    for (int i = k + 1; i < NF; ++i) {
+      const double li = sh.vec[i];
+      double* Hi = H + (int64_t)i * ld;
+      for (int j = k + 1 + tid; j <= i; j += WT) Hi[j] = fma(-li, sh.vec[j], Hi[j]);
+    }
+    gfence();
+    __syncthreads();
+  }
+  // ---------------- 5: J = L^-T (row c of J = column c of L^-1) -------------
+  if (status == ST_SOLVED) {
+    for (int c = tid; c < NF; c += WT) {
+      double* Jc = J + (int64_t)c * ld;
+      for (int i = 0; i < c; ++i) Jc[i] = 0.0;
+      for (int i = c; i < NF; ++i) {
+        const double* Li = H + (int64_t)i * ld;
+        double acc = (i == c) ? 1.0 : 0.0;
+        for (int k = c; k < i; ++k) acc = fma(-Li[k], Jc[k], acc);
+        Jc[i] = acc / Li[i];
+      }
+    }
+    gfence();
+    __syncthreads();
+  }
+  // ---------------- 6: Goldfarb-Idnani -------------------------------------
+  int iters = 0;
+  const double mu = a.mu ? a.mu[b] : a.mu_default;
+  const double zc = dt * dtm;   // coefficient scale of fz_j in z_k (Bd[8][2] = dt/m)
+  if (xin[2] - kZmin < -kTol || zb[1] - kZmin < -kTol) status = ST_INFEAS;   // constant rows z_0, z_1
+  if (status == ST_SOLVED) {
+    // x = -J J' h
+    for (int i = tid; i < NF; i += WT) {
+      double acc = 0.0;
+      for (int k = 0; k <= i; ++k) acc = fma(J[(int64_t)k * ld + i], hv[k], acc);
+      sh.vec[i] = acc;
+    }
+    for (int i = tid; i < 4 * NV; i += WT) isa[i] = 0;
+    __syncthreads();
+    rows_dot(J, ld, NF, 0, sh.vec, xv);
+    gfence();
+    __syncthreads();
+    for (int i = tid; i < NF; i += WT) xv[i] = -xv[i];
+    gfence();
+    __syncthreads();
+  }
+  int q = 0;
+  const int max_iter = 4 * NV + 50;
+  bool done = status != ST_SOLVED;
+  while (!done) {
+    // ---- slacks of every constraint; the most violated one ----
+    double best = INFINITY;
+    int bid = 0x7fffffff;
+    for (int v = tid; v < NV; v += WT) {
+      const int j = v / 6, c = v - 6 * j;
+      const bool stance = cc[j] != 0.0;
+      const double xvv = pos[v] >= 0 ? xv[pos[v]] : 0.0;
+      double s0 = INFINITY, s1 = INFINITY, s2 = INFINITY;
+      if (c >= 3) {
+        const double lim = tau_lim(c);
+        s0 = xvv + lim;
+        s1 = lim - xvv;
+        if (c == 3 && j >= 2) {
+          double z1 = 0.0, n2 = 0.0;
+          for (int jj = 0; jj <= j - 2; ++jj) {
+            if (cc[jj] == 0.0) continue;
+            const double cz = zc * (double)(j - 1 - jj);
+            z1 = fma(cz, xv[pos[6 * jj + 2]], z1);
+            n2 = fma(cz, cz, n2);
+          }
+          const double zrow = (zb[j] - kZmin) + z1;
+          s2 = n2 > 0.0 ? zrow / sqrt(n2) : ((zrow < -kTol) ? -INFINITY : INFINITY);
+        }
+      } else if (stance && !(VAR == 2 && c == 1)) {
+        const double fz = xv[pos[6 * j + 2]];
+        if (c == 2) {
+          s0 = fz;
+          s1 = kFzMax - fz;
+        } else {
+          const double inv = 1.0 / sqrt(1.0 + mu * mu);
+          s0 = (mu * fz - xvv) * inv;
+          s1 = (mu * fz + xvv) * inv;
+        }
+      }
+      if (!isa[4 * v]) argmin_combine(best, bid, s0, 4 * v);
+      if (!isa[4 * v + 1]) argmin_combine(best, bid, s1, 4 * v + 1);
+      if (!isa[4 * v + 2]) argmin_combine(best, bid, s2, 4 * v + 2);
+    }
+    block_argmin(best, bid, sh);
+    if (!(best < -kTol)) break;   // primal feasible: optimal
+    const int p = bid;
+    // n_p as (free index, coefficient) pairs and its rhs b_p
+    if (tid == 0) {
+      const int v = p >> 2, sl = p & 3, j = v / 6, c = v - 6 * j;
+      int n = 0;
+      double bp = 0.0;
+      if (c >= 3) {
+        if (sl < 2) {
+          sh.npi[n] = pos[v]; sh.npv[n++] = sl == 0 ? 1.0 : -1.0;
+          bp = -tau_lim(c);
+        } else {
+          for (int jj = 0; jj <= j - 2; ++jj)
+            if (cc[jj] != 0.0) { sh.npi[n] = pos[6 * jj + 2]; sh.npv[n++] = zc * (double)(j - 1 - jj); }
+          bp = kZmin - zb[j];
+        }
+      } else if (c == 2) {
+        sh.npi[n] = pos[v]; sh.npv[n++] = sl == 0 ? 1.0 : -1.0;
+        bp = sl == 0 ? 0.0 : -kFzMax;
+      } else {
+        sh.npi[n] = pos[v]; sh.npv[n++] = sl == 0 ? -1.0 : 1.0;
+        sh.npi[n] = pos[6 * j + 2]; sh.npv[n++] = mu;
+      }
+      sh.npn = n;
+      sh.bp = bp;
+    }
+    __syncthreads();
+    const int npn = sh.npn;
+    const double bp = sh.bp;
+    double uplus = 0.0;
+    while (true) {
+      if (++iters > max_iter) { status = ST_MAXIT; done = true; break; }
+      // d = J' n_p (a combination of <= N rows of J)
+      for (int i = tid; i < NF; i += WT) {
+        double acc = 0.0;
+        for (int e = 0; e < npn; ++e) acc = fma(sh.npv[e], J[(int64_t)sh.npi[e] * ld + i], acc);
+        sh.vec[i] = acc;
+        dv[i] = acc;
+      }
+      __syncthreads();
+      // z = J2 d2, |d2|^2, |d|^2
+      rows_dot(J, ld, NF, q, sh.vec, zv);
+      double zz = 0.0, dd = 0.0;
+      for (int i = tid; i < NF; i += WT) {
+        const double di = sh.vec[i];
+        dd = fma(di, di, dd);
+        if (i >= q) zz = fma(di, di, zz);
+      }
+      zz = block_sum(zz, sh);
+      dd = block_sum(dd, sh);
+      gfence();
+      __syncthreads();
+      // r = R^-1 d1, the drop candidate and n_p' x - b_p (q, n_p small: one thread)
+      if (tid == 0) {
+        for (int i = q - 1; i >= 0; --i) {
+          double t = sh.vec[i];
+          for (int k = i + 1; k < q; ++k) t = fma(-Rm[(int64_t)i * ld + k], rv[k], t);
+          rv[i] = t / Rm[(int64_t)i * ld + i];
+        }
+        double t1 = INFINITY;
+        int kd = -1;
+        for (int j = 0; j < q; ++j)
+          if (rv[j] > 0.0 && ua[j] / rv[j] < t1) { t1 = ua[j] / rv[j]; kd = j; }
+        double sp = -bp;
+        for (int e = 0; e < npn; ++e) sp = fma(sh.npv[e], xv[sh.npi[e]], sp);
+        sh.t1 = t1;
+        sh.kd = kd;
+        sh.sp = sp;
+      }
+      gfence();
+      __syncthreads();
+      const double t1 = sh.t1, sp = sh.sp;
+      const int kd = sh.kd;
+      const bool has_z = zz > 1e-24 * dd;
+      const double t2 = has_z ? -sp / zz : INFINITY;   // n_p' z = |d2|^2
+      const double t = t1 < t2 ? t1 : t2;
+      if (!(t < INFINITY)) { status = ST_INFEAS; done = true; break; }
+      if (has_z)
+        for (int i = tid; i < NF; i += WT) xv[i] = fma(t, zv[i], xv[i]);
+      if (tid == 0)
+        for (int j = 0; j < q; ++j) ua[j] = fma(-t, rv[j], ua[j]);
+      uplus += t;
+      gfence();
+      __syncthreads();
+      if (has_z && t == t2) {
+        // ---- add p: one Householder reflection maps d2 onto alpha e_q ----
+        const double dq = sh.vec[q];
+        const double alpha = sqrt(zz);
+        const double sg = dq >= 0.0 ? 1.0 : -1.0;
+        const double beta = 1.0 / (alpha * (alpha + fabs(dq)));   // 2 / v'v
+        for (int k = q + tid; k < NF; k += WT) sh.vec2[k] = (k == q) ? dq + sg * alpha : sh.vec[k];
+        __syncthreads();
+        rows_dot(J, ld, NF, q, sh.vec2, wv);   // w = J2 v
+        gfence();
+        __syncthreads();
+        // J2 <- J2 (I - beta v v'); column q flips sign when sg > 0 so that
+        // the new R diagonal is +alpha
+        for (int i = 0; i < NF; ++i) {
+          double* Ji = J + (int64_t)i * ld;
+          const double bwi = beta * wv[i];
+          for (int k = q + tid; k < NF; k += WT) {
+            double x = fma(-bwi, sh.vec2[k], Ji[k]);
+            if (k == q && sg > 0.0) x = -x;
+            Ji[k] = x;
+          }
+        }
+        for (int i = tid; i < q; i += WT) Rm[(int64_t)i * ld + q] = sh.vec[i];
+        if (tid == 0) {
+          Rm[(int64_t)q * ld + q] = alpha;
+          act[q] = p;
+          ua[q] = uplus;
+          isa[p] = 1;
+        }
+        ++q;
+        gfence();
+        __syncthreads();
+        break;
+      }
+      // ---- drop kd: delete column kd of R, restore the triangle ----
+      if (tid == 0) {
+        isa[act[kd]] = 0;
+        for (int j = kd; j < q - 1; ++j) {
+          act[j] = act[j + 1];
+          ua[j] = ua[j + 1];
+          for (int i = 0; i <= j + 1; ++i) Rm[(int64_t)i * ld + j] = Rm[(int64_t)i * ld + j + 1];
+        }
+      }
+      gfence();
+      __syncthreads();
+      for (int j = kd; j < q - 1; ++j) {
+        if (tid == 0) {
+          const double aa = Rm[(int64_t)j * ld + j], bb = Rm[(int64_t)(j + 1) * ld + j];
+          const double hh = sqrt(aa * aa + bb * bb);
+          double c = 1.0, s = 0.0;
+          if (hh != 0.0) { c = aa / hh; s = bb / hh; }
+          for (int k = j; k < q - 1; ++k) {
+            const double r0 = Rm[(int64_t)j * ld + k], r1 = Rm[(int64_t)(j + 1) * ld + k];
+            Rm[(int64_t)j * ld + k] = c * r0 + s * r1;
+            Rm[(int64_t)(j + 1) * ld + k] = -s * r0 + c * r1;
+          }
+          sh.gc = c;
+          sh.gs = s;
+        }
+        gfence();
+        __syncthreads();
+        const double c = sh.gc, s = sh.gs;
+        for (int i = tid; i < NF; i += WT) {
+          double* Ji = J + (int64_t)i * ld;
+          const double x0 = Ji[j], x1 = Ji[j + 1];
+          Ji[j] = c * x0 + s * x1;
+          Ji[j + 1] = -s * x0 + c * x1;
+        }
+        gfence();
+        __syncthreads();
+      }
+      if (tid == 0)
+        for (int i = 0; i < q; ++i) Rm[(int64_t)i * ld + q - 1] = 0.0;
+      --q;
+      gfence();
+      __syncthreads();
+    }
+  }
+  // ---------------- 7: outputs ---------------------------------------------
+  for (int v = tid; v < NV; v += WT) {
+    const double u = (status == ST_SOLVED && pos[v] >= 0) ? xv[pos[v]] : 0.0;
+    uo[v] = u;
+    a.u[b * NV + v] = u;
+  }
+  gfence();
+  __syncthreads();
+  double* xo = a.x ? a.x + b * 12 * (N + 1) : nullptr;
+  if (tid < 64) {
+    double xrr = tid < 12 ? xin[tid] : 0.0;
+    if (xo && tid < 12) xo[tid] = xrr;
+    const double qr = qdiag(tid);
+    const int rw = (tid >= 9 && tid < 12) ? tid - 9 : 0;
+    const int rvv = (tid >= 6 && tid < 9) ? tid - 6 : 0;
+    double objl = 0.0;
+    for (int k = 0; k < N; ++k) {
+      const double cp = cs[2 * k], sp = cs[2 * k + 1];
+      const double* bwr = bw + 18 * k + 6 * rw;
+      const double* uk = uo + 6 * k;
+      double bw_u = 0.0;
+      for (int c = 0; c < 6; ++c) bw_u = fma(bwr[c], uk[c], bw_u);
+      double bv_u;
+      if constexpr (VAR == 3) {
+        bv_u = dtm * uk[rvv];
+      } else {   // Rz' dt/m
+        const double u0 = uk[0], u1 = uk[1], u2 = uk[2];
+        bv_u = (rvv == 0) ? dtm * (cp * u0 - sp * u1) : ((rvv == 1) ? dtm * (sp * u0 + cp * u1) : dtm * u2);
+      }
+      const double bu = (tid >= 9 && tid < 12) ? bw_u : ((tid >= 6 && tid < 9) ? bv_u : 0.0);
+      xrr = ad_lane(xrr, dt, cp, sp) + bu + ((tid == 8) ? -a.g * dt : 0.0);
+      const double kf = (k == N - 1) ? kTermQ : 1.0;
+      const double e = xrr - (tid < 12 ? xr[12 * k + tid] : 0.0);
+      objl = fma(kf * qr * e, e, objl);
+      if (k < N - 1 && tid < 6) {
+        const double ubz = a.uref_aliased ? ((cc[N - 1] != 0.0) ? 2.0 * a.m * a.g : 0.0)
+                                          : ((cc[k] != 0.0) ? 2.0 * a.m * a.g : 0.0);
+        const double du = uk[tid] - (tid == 2 ? ubz : 0.0);
+        objl = fma(kRdiag * du, du, objl);
+      }
+      if (xo && tid < 12) xo[12 * (k + 1) + tid] = xrr;
+    }
+    const double objv = wave_sum(objl);
+    if (tid == 0) {
+      if (a.obj) a.obj[b] = objv;
+      a.status[b] = status;
+      if (a.iters) a.iters[b] = iters;
+    }
+  }
+}
+
+template <int VAR>
+__global__ void __launch_bounds__(WT, 2) wide_kernel(SolveArgs a, int N) {
+  __shared__ Shared sh;
+  double* ws = a.ws + (int64_t)blockIdx.x * a.ws_stride;
+  for (int64_t b = blockIdx.x; b < a.B; b += gridDim.x) {
+    wide_solve<VAR>(a, N, b, ws, sh);
+    gfence();
+    __syncthreads();
+  }
+}
+
+}  // namespace
+
+bool launch_solve_wide(int variant, int N, const SolveArgs& a, hipStream_t s) {
+  if (N < 1 || N > kWideNmax || !a.ws || a.ws_groups < 1) return false;
+  if (a.B <= 0) return true;
+  const int64_t g = a.B < a.ws_groups ? a.B : a.ws_groups;
+  if (variant == 3) {
+    hipLaunchKernelGGL((wide_kernel<3>), dim3((unsigned)g), dim3(WT), 0, s, a, N);
+    return true;
+  }
+  if (variant == 2) {
+    hipLaunchKernelGGL((wide_kernel<2>), dim3((unsigned)g), dim3(WT), 0, s, a, N);
+    return true;
+  }
+  return false;
+}
+
+}  // namespace hmpc

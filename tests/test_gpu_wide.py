@@ -1,0 +1,136 @@
+"""GPU parity of the generic-horizon kernel (hmpc_wide.hip): horizons without
+a dedicated kernel, including the Runner's default N = 60
+(src/robotrunner.py:46), through the C ABI.
+
+Checker: the oracle's C port (oracle/hmpc_port.c, pinned to the reference's
+build_qp fixtures by tests/test_oracle_port.py) on every instance, and the
+numpy oracle (exact QP of the reference-built problem) on a few.  Same
+tolerances as tests/test_gpu_parity.py: |u* - u*_oracle| <= 1e-6,
+|obj - obj_oracle| <= 1e-9 |obj|, equal statuses.
+"""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip('torch')
+
+pytestmark = pytest.mark.gpu
+
+U_TOL = 1e-6
+OBJ_RTOL = 1e-9
+
+
+@pytest.fixture(scope='module')
+def hm():
+    if not torch.cuda.is_available():
+        pytest.fail('GPU tests need an MI355X (torch.cuda.is_available() is False)')
+    import hmpc
+    return hmpc
+
+
+def ctx_for(hm, variant, N, uref='aliased'):
+    from oracle import hmpc_oracle as ho
+    c = ho.runner_constants()
+    return hm.Context(variant, N, t=c['t'], m=c['m'], g=c['g'], mu=1.0, Jinv=c['Jinv'], rh=c['rh'],
+                      uref_mode=uref)
+
+
+def port_solve(variant, N, inst, uref='aliased'):
+    from oracle import port
+    return port.solve_batch(variant, N, inst['x_in'], inst['x_lin'], inst['x_ref'], inst['pf'],
+                            inst['C'], mu=inst['mu'], uref_mode=uref, nthreads=8)
+
+
+def check(gpu, ref):
+    ok = ref['status'] == 0
+    assert np.array_equal(gpu['status'] == 0, ok), (gpu['status'], ref['status'])
+    du = np.abs(gpu['u'][ok] - ref['u'][ok]).max(initial=0.0)
+    dob = (np.abs(gpu['obj'][ok] - ref['obj'][ok]) / np.abs(ref['obj'][ok])).max(initial=0.0)
+    assert du <= U_TOL, du
+    assert dob <= OBJ_RTOL, dob
+    return du
+
+
+@pytest.mark.parametrize('variant,N,curve,musweep', [
+    ('3f', 7, True, False), ('2f', 13, False, True), ('3f', 30, True, True),
+    ('3f', 60, False, False), ('3f', 60, True, True), ('2f', 60, True, False)])
+def test_wide_kernel_matches_port(hm, variant, N, curve, musweep):
+    import hmpc_plan as hp
+    B = 48
+    inst = hp.sample_instances(B, N, curve=curve, seed=100 + N, mu_sweep=(0.3, 1.2) if musweep else None)
+    cx = ctx_for(hm, variant, N)
+    gpu = cx.solve_host(inst['x_in'], inst['x_lin'], inst['x_ref'], inst['pf'], inst['C'],
+                        mu=inst['mu'])
+    cx.close()
+    ref = port_solve(variant, N, inst)
+    assert (ref['status'] == 0).mean() > 0.9
+    check(gpu, ref)
+
+
+@pytest.mark.parametrize('uref', ['aliased', 'per_stage'])
+def test_wide_kernel_matches_numpy_oracle_n60(hm, uref):
+    """Two N=60 instances against the pinned numpy oracle (exact optimum of
+    the reference-built QP, both u_ref semantics)."""
+    import hmpc_plan as hp
+    from oracle import hmpc_oracle as ho
+    N = 60
+    inst = hp.sample_instances(2, N, curve=True, seed=61)
+    cx = ctx_for(hm, '3f', N, uref)
+    gpu = cx.solve_host(inst['x_in'], inst['x_lin'], inst['x_ref'], inst['pf'], inst['C'],
+                        mu=inst['mu'])
+    cx.close()
+    p = ho.MpcParams.runner('3f', N)
+    for i in range(2):
+        r = ho.solve_instance(p, inst['x_in'][i], inst['x_lin'][i], inst['x_ref'][i], inst['pf'][i],
+                              inst['C'][i], uref)
+        assert r['status'] == 'solved' and gpu['status'][i] == 0
+        assert np.abs(gpu['u'][i] - r['u']).max() <= U_TOL
+        assert abs(gpu['obj'][i] - r['obj']) <= OBJ_RTOL * abs(r['obj'])
+        np.testing.assert_allclose(gpu['x'][i], r['x'], rtol=0, atol=1e-6)
+
+
+def test_wide_kernel_persistent_groups_and_batch_invariance(hm):
+    """More instances than resident workgroups (each workgroup loops over
+    instances, reusing its workspace): every row equals the same instance
+    solved alone, bitwise, and matches the port."""
+    import hmpc_plan as hp
+    N, B = 7, 1100
+    inst = hp.sample_instances(B, N, curve=True, seed=9, mu_sweep=(0.3, 1.2))
+    cx = ctx_for(hm, '3f', N)
+    gpu = cx.solve_host(inst['x_in'], inst['x_lin'], inst['x_ref'], inst['pf'], inst['C'],
+                        mu=inst['mu'])
+    sub = {k: v[1037:1040] for k, v in inst.items()}
+    one = cx.solve_host(sub['x_in'], sub['x_lin'], sub['x_ref'], sub['pf'], sub['C'], mu=sub['mu'])
+    cx.close()
+    np.testing.assert_array_equal(gpu['u'][1037:1040], one['u'])
+    check(gpu, port_solve('3f', N, inst))
+
+
+def test_wide_kernel_infeasible_and_empty(hm):
+    import hmpc_plan as hp
+    N = 30
+    inst = hp.sample_instances(4, N, curve=False, seed=4)
+    inst['x_in'][1, 2] = 0.05          # below z >= 0.1 at stage 0: infeasible
+    inst['x_lin'][1, 0, 2] = 0.05
+    cx = ctx_for(hm, '3f', N)
+    gpu = cx.solve_host(inst['x_in'], inst['x_lin'], inst['x_ref'], inst['pf'], inst['C'],
+                        mu=inst['mu'])
+    ref = port_solve('3f', N, inst)
+    assert gpu['status'][1] != 0 and ref['status'][1] != 0
+    check(gpu, ref)
+    e = cx.solve_host(inst['x_in'][:0], inst['x_lin'][:0], inst['x_ref'][:0], inst['pf'][:0],
+                      inst['C'][:0])
+    assert e['u'].shape == (0, N, 6)
+    cx.close()
+
+
+def test_dropin_mpc_n60_closed_loop_matches_oracle(hm):
+    """The reference Runner's own horizon (N = 60) through the drop-in Runner
+    on the device, against the oracle's closed loop (numpy exact solves)."""
+    import hmpc_runner
+    from oracle import hmpc_plant as pl
+    n = 3
+    r = hmpc_runner.Runner(dyn='3f', curve=False, N_run=2000, N=60, batch=1)
+    out = r.run(n_periods=n)
+    r.close()
+    ref = pl.run_closed_loop(N=60, N_run=2000, curve=False, n_periods=n)
+    np.testing.assert_allclose(out['X_traj'][0], ref['X_traj'], rtol=0, atol=1e-7)
