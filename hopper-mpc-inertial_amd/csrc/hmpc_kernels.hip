@@ -128,6 +128,10 @@ __device__ __forceinline__ void lds_wait(dbl2& a, dbl2& b) {
   asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(a), "+v"(b) : "i"(CNT));
 }
 template <int CNT>
+__device__ __forceinline__ void lds_wait(double& a, double& b) {
+  asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(a), "+v"(b) : "i"(CNT));
+}
+template <int CNT>
 __device__ __forceinline__ void lds_wait(double& a) {
   asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(a) : "i"(CNT));
 }
@@ -136,13 +140,13 @@ template <int W>
 struct Blk {
   // LDS ordering point.  One wave: LDS instructions of a wave execute in
   // order, so only the compiler has to be kept from reordering them.
-  __device__ static void sync() {
+  __device__ __forceinline__ static void sync() {
     if constexpr (W == 1) __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     else __syncthreads();
   }
   // `red` must hold >= 2*W doubles; calls are bracketed by barriers (W > 1)
   // so consecutive calls may reuse it.
-  __device__ static double sum(double x, double* red) {
+  __device__ __forceinline__ static double sum(double x, double* red) {
     x = wave_sum(x);
     if constexpr (W == 1) {
       return x;
@@ -156,7 +160,7 @@ struct Blk {
       return s;
     }
   }
-  __device__ static void argmin(double& v, int& i, double* red) {
+  __device__ __forceinline__ static void argmin(double& v, int& i, double* red) {
     wave_argmin(v, i);
     if constexpr (W > 1) {
       __syncthreads();
@@ -172,7 +176,7 @@ struct Blk {
     }
   }
   // value of x in lane l (l uniform)
-  __device__ static double bcast(double x, int l, double* red) {
+  __device__ __forceinline__ static double bcast(double x, int l, double* red) {
     if constexpr (W == 1) {
       return rdlane(x, l);
     } else {
@@ -183,7 +187,7 @@ struct Blk {
     }
   }
   // first lane (over the workgroup) with flag set, or -1
-  __device__ static int first(bool flag, double* red) {
+  __device__ __forceinline__ static int first(bool flag, double* red) {
     unsigned long long m = __ballot(flag);
     int f = m ? (int)__builtin_ctzll(m) + (int)(threadIdx.x & ~63u) : 0x7fffffff;
     if constexpr (W > 1) {
@@ -231,7 +235,8 @@ struct Lay {
   static constexpr int GV = CB + QMAX;             // [QMAX][2] Givens of a drop
   static constexpr int SD = GV + 2 * QMAX;         // [QMAX] subdiagonal scratch
   static constexpr int RM = SD + QMAX;             // packed upper R, col l at l(l+1)/2
-  static constexpr int GEND = RM + e2(QMAX * (QMAX + 1) / 2);
+  static constexpr int GS = RM + e2(QMAX * (QMAX + 1) / 2);   // [W][QMAX] Gram-Schmidt partials (W > 1)
+  static constexpr int GEND = GS + (W > 1 ? W * QMAX : 0);
   static constexpr int COLB = G0;                  // [2][NT+8] (phase 4 only), 16-B aligned
   static_assert((G0 & 1) == 0, "column buffers must be 16-B aligned");
   static constexpr int U0 = (GEND > COLB + 2 * (NT + 8)) ? GEND : COLB + 2 * (NT + 8);
@@ -262,6 +267,16 @@ __device__ __forceinline__ int loff(int r) { return (r * (r + 1)) >> 1; }
 // column k.  L^-1 b = diag(1/L) M^-1 b and L^-T b = M^-T (diag(1/L) b): one
 // step's dependent chain is just readlane -> fma.
 // ----------------------------------------------------------------------------
+// Two-wave sweeps: every wave gets all NV entries of the right-hand side
+// (rows lane and lane + 64).  `red` must hold NT doubles here (the XS row).
+__device__ __forceinline__ void sweep_stage(double b, double& a0, double& a1, double* buf) {
+  const int lane = threadIdx.x & 63;
+  __syncthreads();
+  buf[threadIdx.x] = b;
+  __syncthreads();
+  a0 = buf[lane];
+  a1 = buf[lane + 64];
+}
 // y = L^-1 b (lane v holds b_v), M from registers, fully unrolled.
 // Mr[s] = M[tid][s] below the diagonal and 0 on and above it.
 template <int N>
@@ -311,11 +326,44 @@ __device__ __forceinline__ double tri_fwd_lds(double acc, const double* Mc, cons
     }
     lds_wait<0>(ring[0]);   // drain the ring (its last loads are dummies)
   } else {
+    static_assert(L::W == 2 && NV > 64, "two-wave sweeps only");
+    // Every wave runs the whole sweep on all NV rows (two per lane: lane and
+    // lane + 64) instead of exchanging one value per step through LDS and a
+    // barrier; wave w keeps the rows it owns.  Loads run 4 steps ahead.
+    const int lane = tid & 63;
+    double a0, a1;
+    sweep_stage(acc, a0, a1, red);
+    const unsigned b0 = lds_addr(Mc + lane), b1 = lds_addr(Mc + lane + 64), zaddr = lds_addr(zero);
+    auto ad0 = [&](int s) -> unsigned {
+      return (lane > s && s < NV) ? b0 + 8u * (unsigned)(L::cb(s) - s) : zaddr;
+    };
+    auto ad1 = [&](int s) -> unsigned {
+      return (lane + 64 > s && lane + 64 < NV && s < NV) ? b1 + 8u * (unsigned)(L::cb(s) - s) : zaddr;
+    };
+    double r0[4], r1[4];
+    sfor<0, 4>([&](auto jc) __attribute__((always_inline)) {
+      constexpr int j = decltype(jc)::value;
+      lds_ld64(r0[j], ad0(j));
+      lds_ld64(r1[j], ad1(j));
+    });
+    auto steps = [&](int s, const double& src, int off) __attribute__((always_inline)) {
+      sfor<0, 4>([&](auto jc) __attribute__((always_inline)) {
+        constexpr int j = decltype(jc)::value;
+        const int sj = s + j;
+        const double ys = rdlane(src, sj - off);
+        lds_wait<6>(r0[j], r1[j]);
+        a0 = fma(-r0[j], ys, a0);
+        a1 = fma(-r1[j], ys, a1);
+        lds_ld64(r0[j], ad0(sj + 4));
+        lds_ld64(r1[j], ad1(sj + 4));
+      });
+    };
 #pragma unroll 1
-    for (int s = 0; s < NV; ++s) {
-      const double l = *((tid > s && tid < NV) ? Mc + L::cb(s) + (tid - s) : zero);
-      acc = fma(-l, Blk<L::W>::bcast(acc, s, red), acc);
-    }
+    for (int s = 0; s < 64; s += 4) steps(s, a0, 0);
+#pragma unroll 1
+    for (int s = 64; s < SEND; s += 4) steps(s, a1, 64);
+    lds_wait<0>(r0[0], r1[0]);   // drain the ring (its last loads are dummies)
+    acc = tid < 64 ? a0 : a1;
   }
   // lane v's accumulator is final once step v has read it
   return acc * dinv;
@@ -354,14 +402,42 @@ __device__ __forceinline__ double tri_bwd(double acc, const double* Mc, const do
     }
     lds_wait<0>(ring[0]);   // drain the ring (its last loads are dummies)
   } else {
-    auto addr = [&](int s) -> const double* {
-      return (tid < s && s < NV && s >= 0) ? Mc + cbt + (s - tid) : zero;
+    static_assert(L::W == 2 && NV > 64, "two-wave sweeps only");
+    // as in tri_fwd_lds: each wave sweeps all rows (lane, lane + 64)
+    const int lane = tid & 63;
+    double a0, a1;
+    sweep_stage(acc, a0, a1, red);
+    const unsigned b0 = lds_addr(Mc + L::cb(lane) - lane);
+    const unsigned b1 = lds_addr(Mc + (lane + 64 < NV ? L::cb(lane + 64) - (lane + 64) : 0));
+    const unsigned zaddr = lds_addr(zero);
+    auto ad0 = [&](int s) -> unsigned { return (lane < s && s < NV && s >= 0) ? b0 + 8u * (unsigned)s : zaddr; };
+    auto ad1 = [&](int s) -> unsigned {
+      return (lane + 64 < s && s < NV && s >= 0) ? b1 + 8u * (unsigned)s : zaddr;
+    };
+    double r0[4], r1[4];
+    sfor<0, 4>([&](auto jc) __attribute__((always_inline)) {
+      constexpr int j = decltype(jc)::value;
+      lds_ld64(r0[j], ad0(STOP - j));
+      lds_ld64(r1[j], ad1(STOP - j));
+    });
+    auto steps = [&](int s, const double& src, int off) __attribute__((always_inline)) {
+      sfor<0, 4>([&](auto jc) __attribute__((always_inline)) {
+        constexpr int j = decltype(jc)::value;
+        const int sj = s - j;
+        const double zs = rdlane(src, sj - off);
+        lds_wait<6>(r0[j], r1[j]);
+        a0 = fma(-r0[j], zs, a0);
+        a1 = fma(-r1[j], zs, a1);
+        lds_ld64(r0[j], ad0(sj - 4));
+        lds_ld64(r1[j], ad1(sj - 4));
+      });
     };
 #pragma unroll 1
-    for (int s = STOP; s >= 0; --s) {
-      const double l = *addr(s);
-      acc = fma(-l, Blk<L::W>::bcast(acc, s, red), acc);
-    }
+    for (int s = STOP; s >= 64; s -= 4) steps(s, a1, 64);
+#pragma unroll 1
+    for (int s = 63; s >= 0; s -= 4) steps(s, a0, 0);
+    lds_wait<0>(r0[0], r1[0]);
+    acc = tid < 64 ? a0 : a1;
   }
   return acc;   // lane v's accumulator is final once step v has read it
 }
@@ -817,7 +893,9 @@ solve_kernel(SolveArgs a) {
           });
           if (tid >= k && tid < NV) sm[L::LC + L::cb(k) + tid - k] = (tid == k) ? rs : tk;
           mine = nxt;
-          __syncthreads();   // every wave is done with col before step k+2 rewrites it
+          // (no barrier here: a wave rewrites this buffer at step k+2 only
+          // after the barrier of step k+1, which every wave reaches after
+          // its step-k reads)
         }
       });
     }
@@ -833,8 +911,10 @@ solve_kernel(SolveArgs a) {
   // ---------------- phase 5: v0 = -L^-T L^-1 h -------------------------------
   double v = 0.0;
   {
-    const double y = tri_fwd<N>(-xs[tid], Rg, dinv, red);
-    v = tri_bwd<N>(y, Lc, zero, dinv, red);
+    double y;
+    if constexpr (W == 1) y = tri_fwd<N>(-xs[tid], Rg, dinv, red);
+    else y = tri_fwd_lds<N>(-xs[tid], Lc, zero, dinv, xs);   // no per-step exchange
+    v = tri_bwd<N>(y, Lc, zero, dinv, xs);
   }
   HMPC_STAMP(6);
 
@@ -965,7 +1045,7 @@ solve_kernel(SolveArgs a) {
     const double np_me = coef_of(p, tid);
     double u_plus = 0.0;
     // w = L^-1 n_p
-    const double wfull = tri_fwd_lds<N>(np_me, Lc, zero, dinv, red);
+    const double wfull = tri_fwd_lds<N>(np_me, Lc, zero, dinv, xs);
     const double wnorm2 = B::sum(wfull * wfull, red);
 
     // ---- inner loop: step towards satisfying constraint p ----
@@ -977,12 +1057,28 @@ solve_kernel(SolveArgs a) {
       double wp = wfull, zn = wnorm2;
 #pragma unroll 1
       for (int pass = 0; pass < 2 && qu > 0; ++pass) {
-        ladder<0, QMAX>(qu, [&](auto lc) __attribute__((always_inline)) {
-          constexpr int l = decltype(lc)::value;
-          const double cl = B::sum(Qw[l] * wp, red);
-          wp = fma(-cl, Qw[l], wp);
-          if (tid == 0) cbv[l] = (pass == 0) ? cl : cbv[l] + cl;
-        });
+        if constexpr (W == 1) {   // modified Gram-Schmidt: no barriers in one wave
+          ladder<0, QMAX>(qu, [&](auto lc) __attribute__((always_inline)) {
+            constexpr int l = decltype(lc)::value;
+            const double cl = B::sum(Qw[l] * wp, red);
+            wp = fma(-cl, Qw[l], wp);
+            if (tid == 0) cbv[l] = (pass == 0) ? cl : cbv[l] + cl;
+          });
+        } else {   // classical Gram-Schmidt: all q projections behind one exchange
+          double* part = sm + L::GS;
+          ladder<0, QMAX>(qu, [&](auto lc) __attribute__((always_inline)) {
+            constexpr int l = decltype(lc)::value;
+            const double pl = wave_sum(Qw[l] * wp);
+            if ((tid & 63) == 0) part[(tid >> 6) * QMAX + l] = pl;
+          });
+          __syncthreads();
+          ladder<0, QMAX>(qu, [&](auto lc) __attribute__((always_inline)) {
+            constexpr int l = decltype(lc)::value;
+            const double cl = part[l] + part[QMAX + l];
+            wp = fma(-cl, Qw[l], wp);
+            if (tid == 0) cbv[l] = (pass == 0) ? cl : cbv[l] + cl;
+          });
+        }
         const double n2 = B::sum(wp * wp, red);
         const bool enough = n2 > 0.25 * zn;
         zn = n2;
@@ -990,7 +1086,7 @@ solve_kernel(SolveArgs a) {
       }
       B::sync();
       // primal direction z = L^-T w_perp (lane v gets z_v)
-      const double zi = tri_bwd<N>(wp, Lc, zero, dinv, red);
+      const double zi = tri_bwd<N>(wp, Lc, zero, dinv, xs);
       // dual direction r = R^-1 c (lanes l < q), back substitution
       double rcur = tid < qu ? cbv[tid] : 0.0, rmine = 0.0;
       for (int l = qu - 1; l >= 0; --l) {
