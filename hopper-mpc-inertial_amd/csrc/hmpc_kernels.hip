@@ -456,9 +456,6 @@ __device__ __forceinline__ double tri_bwd(double acc, const double* Mc, const do
 #define HMPC_STAMP(i) ((void)0)
 #endif
 
-#ifndef HMPC_CW
-#define HMPC_CW 4
-#endif
 #ifndef HMPC_WAVES_PER_EU
 #define HMPC_WAVES_PER_EU(W) ((W) == 1 ? 2 : 1)
 #endif
@@ -779,65 +776,108 @@ solve_kernel(SolveArgs a) {
       return (NV - lo - 8 * ch) >= 8 ? 4 : (NV - lo - 8 * ch + 1) / 2;
     };
     if constexpr (W == 1) {
+      // Lookahead: step k publishes column k+1 and issues its first load
+      // chunk right after its own first chunk (which holds column k+1), and
+      // does step k+1's pivot arithmetic there, so the LDS round trip and the
+      // pivot chain of step k+1 overlap step k's remaining updates.
+      // Fixed variables (swing forces, 2f fy) are identity rows/columns of H:
+      // their steps update nothing and are skipped (uniform branch on a
+      // ballot of the fixed lanes; 2f fy at compile time).
+      constexpr int CW = 4;   // columns per load chunk
+      auto nldc = [](int ja, int ch) constexpr {   // b128 loads of chunk ch of [ja, NV)
+        return (NV - ja - CW * ch) >= CW ? CW / 2
+                                         : ((NV - ja - CW * ch) > 0 ? (NV - ja - CW * ch + 1) / 2 : 0);
+      };
+      const uint64_t fixmask = __ballot(active_lane && is_fixed(vj3, vc3));
+      dbl2 nb[CW / 2];                 // chunk 0 of the next step
+      double p_rs = 0.0, p_tk = 0.0;   // next step's 1/L_kk and M[tid][k]
+      auto ahead = [&](auto sc) __attribute__((always_inline)) {
+        constexpr int s = decltype(sc)::value;
+        constexpr int JS = (s + 1) & ~1;
+        // lane masks of a step come from an opaque copy of its index: hoisted
+        // out of the unrolled steps they would pin ~100 SGPRs (and spill)
+        const int so = s + opaque_zero();
+        double* col = sm + L::COLB + (s & 1) * (NT + 8);
+        const double mine = Rg[s];
+        col[tid] = (tid >= so && tid < NV) ? mine : 0.0;
+        B::sync();
+        const unsigned cb0 = lds_addr(col + JS);
+        sfor<0, nldc(JS, 0)>([&](auto ic) __attribute__((always_inline)) {
+          constexpr int i = decltype(ic)::value;
+          lds_ld128<16 * i>(nb[i], cb0);
+        });
+        const double piv = rdlane(mine, s);
+        const double pv = piv > 0.0 ? piv : 1.0;
+        nbad += (piv > 0.0) ? 0.0 : 1.0;   // folded into status after the loop
+        pin(nbad);                          // (materialised here, not sunk to the end)
+        p_rs = rsq_nr(pv);
+        p_tk = (mine * p_rs) * p_rs;
+      };
+      ahead(std::integral_constant<int, 0>{});
       sfor<0, NV>([&](auto kc) __attribute__((always_inline)) {
         constexpr int k = decltype(kc)::value;
-        constexpr int JA = (k + 1) & ~1;            // 16-B aligned start of the update
-        constexpr int CW = HMPC_CW;                 // columns per load chunk (4 or 8)
+        constexpr int JA = (k + 1) & ~1;   // 16-B aligned start of the update
         constexpr int NCH = (NV - JA + CW - 1) / CW;
-        // lane masks and addresses of this step are computed from an opaque
-        // copy of k: hoisted out of the unrolled steps they would pin ~100
-        // SGPRs for the whole factorisation (and spill)
+        constexpr int NAHEAD = (k + 1 < NV) ? 1 + nldc((k + 2) & ~1, 0) : 0;   // LDS ops of ahead()
+        constexpr bool kfixed = VAR == 2 && k % 6 == 1;                       // 2f fy
+        constexpr bool kforce = k % 6 < 3;
         const int ko = k + opaque_zero();
-        double* col = sm + L::COLB + (k & 1) * (NT + 8);
-        const double mine = Rg[k];
-        col[tid] = (tid >= ko && tid < NV) ? mine : 0.0;
-        B::sync();
-        const unsigned cbase = lds_addr(col + JA);
-        auto nldc = [](int ch) constexpr {   // b128 loads of chunk ch of [JA, NV)
-          return (NV - JA - CW * ch) >= CW ? CW / 2 : (NV - JA - CW * ch + 1) / 2;
-        };
+        const double rs = p_rs, tk = p_tk;
+        lds_wait<0>(nb[0], nb[1]);   // this step's chunk 0 (and everything older)
+        const bool below = tid > ko && tid < NV;
+        const double nt = below ? -tk : 0.0;
+        // branch-free store of column k of M (other lanes: the column buffer
+        // of step k+1, which ahead() rewrites after this store)
+        {
+          const int o_l = L::LC + L::cb(k) + (tid - ko);
+          const int o_d = L::COLB + ((k + 1) & 1) * (NT + 8) + tid;
+          sm[(tid >= ko && tid < NV) ? o_l : o_d] = (tid == ko) ? rs : tk;
+        }
+        Rg[k] = below ? tk : 0.0;
+        const unsigned cbase = lds_addr(sm + L::COLB + (k & 1) * (NT + 8) + JA);
         dbl2 buf[2][CW / 2];
         auto load = [&](auto chc) __attribute__((always_inline)) {
           constexpr int ch = decltype(chc)::value;
-          if constexpr (ch < NCH) {
-            sfor<0, nldc(ch)>([&](auto ic) __attribute__((always_inline)) {
+          if constexpr (ch >= 1 && ch < NCH) {
+            sfor<0, nldc(JA, ch)>([&](auto ic) __attribute__((always_inline)) {
               constexpr int i = decltype(ic)::value;
               lds_ld128<8 * CW * ch + 16 * i>(buf[ch % 2][i], cbase);
             });
           }
         };
-        load(std::integral_constant<int, 0>{});
-        const double piv = rdlane(mine, k);
-        const double pv = piv > 0.0 ? piv : 1.0;
-        nbad += (piv > 0.0) ? 0.0 : 1.0;   // folded into status after the loop
-        pin(nbad);                          // (materialised here, not sunk to the end)
-        const double rs = rsq_nr(pv);
-        const double tk = (mine * rs) * rs;   // M[tid][k]
-        const bool below = tid > ko && tid < NV;
-        const double nt = below ? -tk : 0.0;
-        sfor<0, NCH>([&](auto chc) __attribute__((always_inline)) {
+        auto update = [&](auto chc, const dbl2 (&bf)[CW / 2]) __attribute__((always_inline)) {
           constexpr int ch = decltype(chc)::value;
-          load(std::integral_constant<int, ch + 1>{});
-          constexpr int younger = ch + 1 < NCH ? nldc(ch + 1) : 0;
-          if constexpr (CW == 8)
-            lds_wait<younger>(buf[ch % 2][0], buf[ch % 2][1], buf[ch % 2][2], buf[ch % 2][3]);
-          else
-            lds_wait<younger>(buf[ch % 2][0], buf[ch % 2][1]);
           sfor<0, CW>([&](auto ic) __attribute__((always_inline)) {
             constexpr int i = decltype(ic)::value;
             constexpr int j = JA + CW * ch + i;
             if constexpr (j > k && j < NV) {
-              const double cv = (i & 1) ? buf[ch % 2][i / 2].y : buf[ch % 2][i / 2].x;
+              const double cv = (i & 1) ? bf[i / 2].y : bf[i / 2].x;
               Rg[j] = fma(nt, cv, Rg[j]);
               pin(Rg[j]);
             }
           });
-        });
-        Rg[k] = below ? tk : 0.0;
-        // branch-free store of column k of M (other lanes: the idle buffer)
-        const int o_l = L::LC + L::cb(k) + (tid - ko);
-        const int o_d = L::COLB + ((k + 1) & 1) * (NT + 8) + tid;
-        sm[(tid >= ko && tid < NV) ? o_l : o_d] = (tid == ko) ? rs : tk;
+        };
+        if constexpr (!kfixed) {
+          const bool run = !kforce || !((fixmask >> k) & 1);   // uniform
+          if (run) {
+            load(std::integral_constant<int, 1>{});
+            if constexpr (NCH > 0) update(std::integral_constant<int, 0>{}, nb);
+          }
+          if constexpr (k + 1 < NV) ahead(std::integral_constant<int, k + 1>{});
+          if (run) {
+            sfor<1, NCH>([&](auto chc) __attribute__((always_inline)) {
+              constexpr int ch = decltype(chc)::value;
+              load(std::integral_constant<int, ch + 1>{});
+              // LDS ops issued after chunk ch's loads: chunk ch+1, and for
+              // ch == 1 also ahead()'s column store and loads
+              constexpr int younger = (ch + 1 < NCH ? nldc(JA, ch + 1) : 0) + (ch == 1 ? NAHEAD : 0);
+              lds_wait<younger>(buf[ch % 2][0], buf[ch % 2][1]);
+              update(chc, buf[ch % 2]);
+            });
+          }
+        } else {
+          if constexpr (k + 1 < NV) ahead(std::integral_constant<int, k + 1>{});
+        }
       });
     } else {
       double mine = Rg[0];   // A[tid][k] of the current step
