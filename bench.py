@@ -33,6 +33,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = 'QP solves/sec (N=10, 3f) at batch=65k, 1→8 MI355X; max |u*−u*_cvxpy|'
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level table)
+FP64_VECTOR_PEAK_TFS = 78.6   # MI355X FP64 vector (half the 157.3 TF FP32 vector rate)
 
 
 def algorithmic_bytes(N, with_mu=True):
@@ -183,12 +184,14 @@ def main():
         bpsolve = algorithmic_bytes(N)
         achieved = bpsolve * B / (kern_ms * 1e-3) / 1e9
         traffic = None
+        flops = None
         tpath = os.path.join(ROOT, 'profiles', 'traffic.json')
         wl = f'{args.variant}_N{N}_B{B}_{"straight" if args.straight else "curve"}' \
              f'{"_musweep" if args.mu_sweep else ""}'
         if os.path.exists(tpath):
             tj = json.load(open(tpath))
             traffic = tj.get(wl, {}).get('bytes_per_launch')
+            flops = tj.get(wl, {}).get('fp64_flops_per_solve')
         total = B * world * args.steps
         rec = {
             'metric': METRIC,
@@ -215,6 +218,12 @@ def main():
                          'kernel': f'hmpc::solve_kernel<{args.variant[0]}, {N}>',
                          'kernel_ms': kern_ms, 'kernel_ms_max_rank': kern_ms_max,
                          'algorithmic_bytes_per_solve': bpsolve, 'solves_per_launch': B},
+            # the bound that matters for this path: executed fp64
+            # VALU flops (rocprofv3 SQ_INSTS_VALU_*_F64 x 64 lanes, profiles/)
+            'fp64_vector': None if flops is None else {
+                'achieved': flops * B / (kern_ms * 1e-3) / 1e12, 'peak': FP64_VECTOR_PEAK_TFS,
+                'unit': 'TFLOP/s', 'frac': flops * B / (kern_ms * 1e-3) / 1e12 / FP64_VECTOR_PEAK_TFS,
+                'flops_per_solve': flops},
             'cpu_baseline': base,
             'solved_frac_min_rank': float(sf[0]),
             'iters_mean': float(it.mean()), 'iters_max': int(it.max()),

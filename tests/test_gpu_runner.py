@@ -178,3 +178,13 @@ def test_runner_batch_rows_are_independent(hm):
     np.testing.assert_array_equal(out['X_traj'][5], out1['X_traj'][0])
     ref = pl.run_closed_loop(N=10, N_run=400, curve=True, n_periods=n, X0=X0[2])
     np.testing.assert_allclose(out['X_traj'][2], ref['X_traj'], rtol=0, atol=1e-7)
+
+
+def test_run_cli_mirror(hm, tmp_path):
+    """hmpc_run.py, the reference run.py's CLI on the device Runner."""
+    import hmpc_run
+    out = tmp_path / 'run.npz'
+    res = hmpc_run.main(['3f', '--N_run', '200', '--N', '10', '--batch', '2', '--out', str(out)])
+    d = np.load(out)
+    assert d['X_traj'].shape == (2, 201, 13) and (res['status'] == 0).all()
+    np.testing.assert_array_equal(d['X_traj'][0], d['X_traj'][1])   # same start state

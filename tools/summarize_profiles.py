@@ -61,6 +61,13 @@ def main(tag):
         tj = json.load(open(tj_path)) if os.path.exists(tj_path) else {}
         tj[wl] = {'bytes_per_launch': fetch + write, 'fetch_bytes': fetch, 'write_bytes': write,
                   'source': f'profiles/{tag}_pmc_summary.json (rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE)'}
+        if 'SQ_INSTS_VALU_FMA_F64' in m:
+            # executed fp64 flops per solve: wave instructions x 64 lanes
+            # (FMA = 2 flops; masked lanes included, so an upper bound)
+            fl = 64.0 * (2 * m['SQ_INSTS_VALU_FMA_F64'] + m.get('SQ_INSTS_VALU_MUL_F64', 0.0)
+                         + m.get('SQ_INSTS_VALU_ADD_F64', 0.0)) / waves
+            tj[wl]['fp64_flops_per_solve'] = fl
+            summary['fp64_flops_per_solve'] = fl
         json.dump(tj, open(tj_path, 'w'), indent=1)
     json.dump(summary, open(os.path.join(dst, f'{tag}_pmc_summary.json'), 'w'), indent=1)
     print(json.dumps(summary, indent=1))
