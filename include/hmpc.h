@@ -70,8 +70,11 @@ typedef struct hmpc_ctx hmpc_ctx;
 /* ABI version (major*10000 + minor*100 + patch) */
 int hmpc_version(void);
 
-/* Which horizons have a compiled kernel for `variant`; writes up to `cap`
-   values into `Ns`, returns the count. */
+/* Which horizons have a dedicated (one- or two-wavefront) kernel for
+   `variant`; writes up to `cap` values into `Ns`, returns the count.  Every
+   other horizon 1 <= N <= 128 (e.g. the Runner's N = 60) is solved by the
+   generic-horizon kernel out of a per-context device workspace; calls on one
+   context are then expected to be stream-ordered. */
 int hmpc_supported_horizons(int variant, int* Ns, int cap);
 
 /* Mpc.__init__: t = MPC sampling time (s), N = horizon, m (kg), g (m/s^2),
