@@ -55,6 +55,9 @@ def parse():
     ap.add_argument('--straight', action='store_true', help='straight plan (default: --curve)')
     ap.add_argument('--mu-sweep', action='store_true', help='mu ~ U(0.3, 1.2)')
     ap.add_argument('--seed', type=int, default=2024)
+    ap.add_argument('--precision', default='f64', choices=['f64', 'f32', 'f64_generic'],
+                    help='configs[4]: f32 = fp32 arithmetic on the generic kernel; '
+                         'f64_generic = its fp64 twin (f64 = the dedicated fp64 kernel)')
     ap.add_argument('--cpu-seconds', type=float, default=10.0,
                     help='budget of the bounded CPU-baseline sample (0 disables)')
     return ap.parse_args()
@@ -127,7 +130,7 @@ def main():
          for k in ('x_in', 'x_lin', 'x_ref', 'pf', 'C', 'mu')}
     c = ho.runner_constants()
     ctx = hmpc.Context(args.variant, N, t=c['t'], m=c['m'], g=c['g'], mu=1.0, Jinv=c['Jinv'],
-                       rh=c['rh'], device=local)
+                       rh=c['rh'], device=local, precision=args.precision)
     out = dict(u=torch.empty((B, N, 6), dtype=torch.float64, device=dev),
                x=torch.empty((B, N + 1, 12), dtype=torch.float64, device=dev),
                obj=torch.empty(B, dtype=torch.float64, device=dev),
@@ -188,7 +191,7 @@ def main():
         tpath = os.path.join(ROOT, 'profiles', 'traffic.json')
         wl = f'{args.variant}_N{N}_B{B}_{"straight" if args.straight else "curve"}' \
              f'{"_musweep" if args.mu_sweep else ""}'
-        if os.path.exists(tpath):
+        if os.path.exists(tpath) and args.precision == 'f64':
             tj = json.load(open(tpath))
             traffic = tj.get(wl, {}).get('bytes_per_launch')
             flops = tj.get(wl, {}).get('fp64_flops_per_solve')
@@ -204,18 +207,19 @@ def main():
             'higher_is_better': True,
             'scaling': 'weak',
             'vs_baseline': None,
-            'dtype': 'f64',
+            'dtype': 'f32' if args.precision == 'f32' else 'f64',
             'data': 'synthetic: Runner path_plan_init plan (--curve) + randomised x0 '
                     '(SURVEY.md 8d), generated on host, resident in HBM before timing',
             'config': {'workload': f'configs[2]: batch={B}/GPU randomised x0 + '
                                    f'{"straight" if args.straight else "--curve"} ref traj, '
                                    f'{args.variant}, horizon N={N}, fp64'
-                                   f'{", mu sweep" if args.mu_sweep else ""}',
+                                   f'{", mu sweep" if args.mu_sweep else ""}'
+                                   f'{"" if args.precision == "f64" else ", " + args.precision + " (generic kernel)"}',
                        'global_batch': B * world, 'horizon': N, 'variant': args.variant,
                        'parallelism': f'shard{world}'},
             'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS,
                          'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic,
-                         'kernel': f'hmpc::solve_kernel<{args.variant[0]}, {N}>',
+                         'kernel': (f'hmpc::solve_kernel<{args.variant[0]}, {N}>' if args.precision == 'f64' else f'hmpc::wide_kernel<{args.variant[0]}, {"float" if args.precision == "f32" else "double"}>'),
                          'kernel_ms': kern_ms, 'kernel_ms_max_rank': kern_ms_max,
                          'algorithmic_bytes_per_solve': bpsolve, 'solves_per_launch': B},
             # the bound that matters for this path: executed fp64

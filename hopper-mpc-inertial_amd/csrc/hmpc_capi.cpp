@@ -23,6 +23,7 @@ struct hmpc_ctx {
   double Jinv[9];
   double rh[3];
   int uref_mode;
+  int precision = HMPC_PREC_F64;
   std::string err;
   // staging buffers (host API) and mpcontrol scratch
   void* dbuf = nullptr;
@@ -66,6 +67,7 @@ hmpc::SolveArgs make_args(hmpc_ctx* c, int64_t B, const double* x_in, const doub
   a.pf_bs = 3 * (int64_t)N; a.pf_rs = 3;
   a.C_bs = N;
   a.ws = nullptr; a.ws_stride = 0; a.ws_groups = 0;
+  a.precision = c->precision;
   return a;
 }
 
@@ -75,7 +77,7 @@ constexpr int kMaxGroups = 512;
 constexpr size_t kWsBudget = (size_t)4 << 30;   // bytes
 
 int prepare_ws(hmpc_ctx* c, int64_t B, hmpc::SolveArgs& a) {
-  if (hmpc::horizon_compiled(c->variant, c->N)) return HMPC_OK;
+  if (c->precision == HMPC_PREC_F64 && hmpc::horizon_compiled(c->variant, c->N)) return HMPC_OK;
   const hmpc::WideLayout Lw(c->N);
   const size_t per = (size_t)Lw.total * sizeof(double);
   int64_t want = B < kMaxGroups ? B : kMaxGroups;
@@ -164,6 +166,16 @@ int hmpc_destroy(hmpc_ctx* c) {
 }
 
 const char* hmpc_last_error(hmpc_ctx* c) { return c ? c->err.c_str() : ""; }
+
+int hmpc_set_precision(hmpc_ctx* c, int precision) {
+  if (!c) return HMPC_ERR_ARG;
+  if (precision != HMPC_PREC_F64 && precision != HMPC_PREC_F32 && precision != HMPC_PREC_F64_GENERIC) {
+    c->err = "unknown precision";
+    return HMPC_ERR_ARG;
+  }
+  c->precision = precision;
+  return HMPC_OK;
+}
 
 int hmpc_solve_batch(hmpc_ctx* c, int64_t B, const double* x_in, const double* x_lin,
                      const double* x_ref, const double* pf, const double* C, const double* mu,

@@ -14,6 +14,7 @@ HMPC_HORIZON_LIST(HMPC_DECL)
 
 bool launch_solve(int variant, int N, const SolveArgs& a, hipStream_t s) {
   if (variant != 2 && variant != 3) return false;
+  if (a.precision != 0) return launch_solve_wide(variant, N, a, s);
 #define HMPC_CASE(n) \
   if (N == n) return launch_solve_n##n(variant, a, s);
   HMPC_HORIZON_LIST(HMPC_CASE)

@@ -37,8 +37,11 @@ struct SolveArgs {
   // global workspace of the generic-horizon kernel (hmpc_wide.hip): one
   // WideLayout(N).total block per resident workgroup
   double* ws;
-  int64_t ws_stride;
+  int64_t ws_stride;   // in elements of the arithmetic type
   int ws_groups;
+  // 0: fp64 (dedicated kernel when the horizon has one), 1: fp32 generic
+  // kernel, 2: fp64 generic kernel (HMPC_PREC_*)
+  int precision;
 };
 
 // Horizons without a dedicated kernel run on the generic kernel up to this N.

@@ -30,22 +30,28 @@ __device__ __forceinline__ double rdlane(double x, int l) {
   int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
   return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
+__device__ __forceinline__ float rdlane(float x, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), l));
+}
 __device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
 
-__device__ __forceinline__ double wave_sum(double x) {
+template <typename R>
+__device__ __forceinline__ R wave_sum(R x) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
   return x;
 }
 
-__device__ __forceinline__ void argmin_combine(double& v, int& i, double v2, int i2) {
+template <typename R>
+__device__ __forceinline__ void argmin_combine(R& v, int& i, R v2, int i2) {
   if (v2 < v || (v2 == v && i2 < i)) { v = v2; i = i2; }
 }
 
-__device__ __forceinline__ void wave_argmin(double& v, int& i) {
+template <typename R>
+__device__ __forceinline__ void wave_argmin(R& v, int& i) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
-    double v2 = __shfl_xor(v, o, 64);
+    R v2 = __shfl_xor(v, o, 64);
     int i2 = __shfl_xor(i, o, 64);
     argmin_combine(v, i, v2, i2);
   }
@@ -57,7 +63,8 @@ __device__ __forceinline__ void wave_argmin(double& v, int& i) {
 //   12..21 roll/pitch block y = (x3, x4, x9, x10):
 //          P00 P01 P11 M00 M01 M10 M11 Q00 Q01 Q11  (M_ij = S[x(3+i)][x(9+j)])
 // f = S e for the structured S (full 12 rows)
-__device__ __forceinline__ void s_times(const double* s, const double (&e)[12], double (&f)[12]) {
+template <typename R>
+__device__ __forceinline__ void s_times(const R* s, const R (&e)[12], R (&f)[12]) {
 #pragma unroll
   for (int a = 0; a < 3; ++a) {
     f[a] = s[3 * a] * e[a] + s[3 * a + 1] * e[6 + a];
@@ -65,7 +72,7 @@ __device__ __forceinline__ void s_times(const double* s, const double (&e)[12], 
   }
   f[5] = s[9] * e[5] + s[10] * e[11];
   f[11] = s[10] * e[5] + s[11] * e[11];
-  const double P00 = s[12], P01 = s[13], P11 = s[14], M00 = s[15], M01 = s[16], M10 = s[17],
+  const R P00 = s[12], P01 = s[13], P11 = s[14], M00 = s[15], M01 = s[16], M10 = s[17],
                M11 = s[18], Q00 = s[19], Q01 = s[20], Q11 = s[21];
   f[3] = P00 * e[3] + P01 * e[4] + M00 * e[9] + M01 * e[10];
   f[4] = P01 * e[3] + P11 * e[4] + M10 * e[9] + M11 * e[10];
@@ -75,19 +82,21 @@ __device__ __forceinline__ void s_times(const double* s, const double (&e)[12], 
 
 // x <- Ad x with Ad = I + dt A(psi): p += dt v; theta += dt Rz(psi) w
 // (src/mpc_cvx_euler_3f.py:27,87,91; rz of src/utils.py:46-51)
-__device__ __forceinline__ void ad_times(double (&x)[12], double dt, double cp, double sp) {
+template <typename R>
+__device__ __forceinline__ void ad_times(R (&x)[12], R dt, R cp, R sp) {
 #pragma unroll
   for (int a = 0; a < 3; ++a) x[a] = fma(dt, x[6 + a], x[a]);
-  const double w0 = x[9], w1 = x[10];
+  const R w0 = x[9], w1 = x[10];
   x[3] = x[3] + ((cp * dt) * w0 + (sp * dt) * w1);
   x[4] = x[4] + ((-sp * dt) * w0 + (cp * dt) * w1);
   x[5] = fma(dt, x[11], x[5]);
 }
 // g <- Ad' g
-__device__ __forceinline__ void adt_times(double (&g)[12], double dt, double cp, double sp) {
+template <typename R>
+__device__ __forceinline__ void adt_times(R (&g)[12], R dt, R cp, R sp) {
 #pragma unroll
   for (int a = 0; a < 3; ++a) g[6 + a] = fma(dt, g[a], g[6 + a]);
-  const double g3 = g[3], g4 = g[4];
+  const R g3 = g[3], g4 = g[4];
   g[9] = g[9] + ((cp * dt) * g3 + (-sp * dt) * g4);
   g[10] = g[10] + ((sp * dt) * g3 + (cp * dt) * g4);
   g[11] = fma(dt, g[5], g[11]);
@@ -96,22 +105,24 @@ __device__ __forceinline__ void adt_times(double (&g)[12], double dt, double cp,
 // The same two maps lane-parallel: lane r < 12 holds component r.  The
 // cross terms come from other lanes (readlane / bpermute); lanes >= 12 pass
 // their value through unchanged.
-__device__ __forceinline__ double ad_lane(double x, double dt, double cp, double sp) {
+template <typename R>
+__device__ __forceinline__ R ad_lane(R x, R dt, R cp, R sp) {
   const int r = threadIdx.x;
-  const double xv = __shfl(x, (int)((threadIdx.x + 6) & 63), 64);   // x[r+6] for r < 3
-  const double w0 = rdlane(x, 9), w1 = rdlane(x, 10), w2 = rdlane(x, 11);
-  double d = 0.0;
+  const R xv = __shfl(x, (int)((threadIdx.x + 6) & 63), 64);   // x[r+6] for r < 3
+  const R w0 = rdlane(x, 9), w1 = rdlane(x, 10), w2 = rdlane(x, 11);
+  R d = R(0);
   d = (r < 3) ? xv : d;
   d = (r == 3) ? (cp * w0 + sp * w1) : d;
   d = (r == 4) ? (cp * w1 - sp * w0) : d;
   d = (r == 5) ? w2 : d;
   return fma(dt, d, x);
 }
-__device__ __forceinline__ double adt_lane(double g, double dt, double cp, double sp) {
+template <typename R>
+__device__ __forceinline__ R adt_lane(R g, R dt, R cp, R sp) {
   const int r = threadIdx.x;
-  const double gv = __shfl(g, (int)((threadIdx.x + 58) & 63), 64);  // g[r-6] for 6 <= r < 9
-  const double g3 = rdlane(g, 3), g4 = rdlane(g, 4), g5 = rdlane(g, 5);
-  double d = 0.0;
+  const R gv = __shfl(g, (int)((threadIdx.x + 58) & 63), 64);  // g[r-6] for 6 <= r < 9
+  const R g3 = rdlane(g, 3), g4 = rdlane(g, 4), g5 = rdlane(g, 5);
+  R d = R(0);
   d = (r >= 6 && r < 9) ? gv : d;
   d = (r == 9) ? (cp * g3 - sp * g4) : d;
   d = (r == 10) ? (sp * g3 + cp * g4) : d;
@@ -123,51 +134,52 @@ __device__ __forceinline__ double qdiag(int r) {   // Q[r][r], 0 beyond the stat
 }
 
 // rows 6..8 of Bd_k, column c2 (< 3): 3f dt/m I (:28), 2f Rz'(psi) dt/m (2f :87)
-template <int VAR>
-__device__ __forceinline__ double bv(int r, int c2, double dtm, double cp, double sp) {
+template <int VAR, typename R>
+__device__ __forceinline__ R bv(int r, int c2, R dtm, R cp, R sp) {
   if constexpr (VAR == 3) {
-    return r == c2 ? dtm : 0.0;
+    return r == c2 ? dtm : R(0);
   } else {
     // Rz' = [[c, -s, 0], [s, c, 0], [0, 0, 1]]
-    if (r == 2 || c2 == 2) return (r == c2) ? dtm : 0.0;
+    if (r == 2 || c2 == 2) return (r == c2) ? dtm : R(0);
     if (r == c2) return cp * dtm;
     return (r == 0) ? -sp * dtm : sp * dtm;
   }
 }
 
 // 2 Bd_j[:, c2]' y[6..11]  (rows 0..5 of Bd are zero)
-template <int VAR>
-__device__ __forceinline__ double bd_dot(int c2, const double (&y)[12], const double* bw, double dtm,
-                                         double cp, double sp) {
-  double acc = 0.0;
+template <int VAR, typename R>
+__device__ __forceinline__ R bd_dot(int c2, const R (&y)[12], const R* bw, R dtm,
+                                         R cp, R sp) {
+  R acc = R(0);
   if (c2 < 3) {
 #pragma unroll
     for (int r = 0; r < 3; ++r) acc = fma(bv<VAR>(r, c2, dtm, cp, sp), y[6 + r], acc);
   }
 #pragma unroll
   for (int r = 0; r < 3; ++r) acc = fma(bw[6 * r + c2], y[9 + r], acc);
-  return 2.0 * acc;
+  return R(2) * acc;
 }
 
 // Mpc.gen_dt_dynamics for stage k (3f :71-94, 2f :70-94): cos/sin of the
 // linearisation yaw and rows 9..11 of Bd_k (rows 6..8 are bv(); the rest of
 // Bd_k is zero).  xlin: [N][12] linearisation rows, pf: [N][3].
-template <int VAR>
-__device__ __forceinline__ void stage_dynamics(int k, const double* xlin, const double* pf,
-                                               const double (&Jinv)[9], const double (&rh)[3], double dt,
-                                               double* cs, double* bwo) {
-  const double psi = xlin[12 * k + 5];
-  double sp, cp;
-  sincos(psi, &sp, &cp);
+template <int VAR, typename R>
+__device__ __forceinline__ void stage_dynamics(int k, const R* xlin, const R* pf,
+                                               const double (&Jinv)[9], const double (&rh)[3], R dt,
+                                               R* cs, R* bwo) {
+  const R psi = xlin[12 * k + 5];
+  R sp, cp;
+  if constexpr (sizeof(R) == 4) sincosf(psi, &sp, &cp);
+  else sincos(psi, &sp, &cp);
   // rz(psi) = [[c, s, 0], [-s, c, 0], [0, 0, 1]]   (src/utils.py:46-51)
-  const double Rz[3][3] = {{cp, sp, 0.0}, {-sp, cp, 0.0}, {0.0, 0.0, 1.0}};
-  double d[3], rf[3];
+  const R Rz[3][3] = {{cp, sp, R(0)}, {-sp, cp, R(0)}, {R(0), R(0), R(1)}};
+  R d[3], rf[3];
 #pragma unroll
   for (int i = 0; i < 3; ++i) d[i] = pf[3 * k + i] - xlin[12 * k + i];
   // rf = rh + Rz (pf - p)   (:84)
 #pragma unroll
-  for (int i = 0; i < 3; ++i) rf[i] = rh[i] + (Rz[i][0] * d[0] + Rz[i][1] * d[1] + Rz[i][2] * d[2]);
-  double T[3][3], Jw[3][3], RzT[3][3];
+  for (int i = 0; i < 3; ++i) rf[i] = R(rh[i]) + (Rz[i][0] * d[0] + Rz[i][1] * d[1] + Rz[i][2] * d[2]);
+  R T[3][3], Jw[3][3], RzT[3][3];
 #pragma unroll
   for (int i = 0; i < 3; ++i)
 #pragma unroll
@@ -177,18 +189,18 @@ __device__ __forceinline__ void stage_dynamics(int k, const double* xlin, const 
   for (int i = 0; i < 3; ++i)
 #pragma unroll
     for (int j = 0; j < 3; ++j)
-      T[i][j] = Rz[i][0] * Jinv[0 * 3 + j] + Rz[i][1] * Jinv[1 * 3 + j] + Rz[i][2] * Jinv[2 * 3 + j];
+      T[i][j] = Rz[i][0] * R(Jinv[0 * 3 + j]) + Rz[i][1] * R(Jinv[1 * 3 + j]) + Rz[i][2] * R(Jinv[2 * 3 + j]);
 #pragma unroll
   for (int i = 0; i < 3; ++i)
 #pragma unroll
     for (int j = 0; j < 3; ++j) Jw[i][j] = T[i][0] * RzT[0][j] + T[i][1] * RzT[1][j] + T[i][2] * RzT[2][j];
-  double Bwt[3][3], Bwf[3][3];
+  R Bwt[3][3], Bwf[3][3];
   // B[9:12, 3:6] = J_w_inv Rz'   (:89)
 #pragma unroll
   for (int i = 0; i < 3; ++i)
 #pragma unroll
     for (int j = 0; j < 3; ++j) Bwt[i][j] = Jw[i][0] * RzT[0][j] + Jw[i][1] * RzT[1][j] + Jw[i][2] * RzT[2][j];
-  double w[3];
+  R w[3];
   if constexpr (VAR == 3) {   // rhat = hat(Rz' rf); B[9:12,0:3] = Jw rhat   (:85,88)
 #pragma unroll
     for (int i = 0; i < 3; ++i) w[i] = RzT[i][0] * rf[0] + RzT[i][1] * rf[1] + RzT[i][2] * rf[2];
@@ -197,7 +209,7 @@ __device__ __forceinline__ void stage_dynamics(int k, const double* xlin, const 
     for (int i = 0; i < 3; ++i) w[i] = rf[i];
   }
   // hat (src/utils.py:21-25)
-  const double hw[3][3] = {{0.0, -w[2], w[1]}, {w[2], 0.0, -w[0]}, {-w[1], w[0], 0.0}};
+  const R hw[3][3] = {{R(0), -w[2], w[1]}, {w[2], R(0), -w[0]}, {-w[1], w[0], R(0)}};
 #pragma unroll
   for (int i = 0; i < 3; ++i)
 #pragma unroll
@@ -207,7 +219,7 @@ __device__ __forceinline__ void stage_dynamics(int k, const double* xlin, const 
       else
         Bwf[i][j] = Bwt[i][0] * hw[0][j] + Bwt[i][1] * hw[1][j] + Bwt[i][2] * hw[2][j];
     }
-  double* bw = bwo + 18 * k;
+  R* bw = bwo + 18 * k;
 #pragma unroll
   for (int i = 0; i < 3; ++i)
 #pragma unroll

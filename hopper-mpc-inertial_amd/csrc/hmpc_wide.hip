@@ -42,33 +42,36 @@ constexpr int WT = 256;               // threads per workgroup
 constexpr int WW = WT / 64;           // waves
 constexpr int NVMAX = 6 * kWideNmax;  // LDS vectors
 
+template <typename T>
 struct Shared {
-  double red[WW];
+  T red[WW];
   int ired[WW];
-  double vec[NVMAX];   // a broadcast vector (Cholesky column, d, Householder v)
-  double vec2[NVMAX];
-  double npv[kWideNmax + 2];   // n_p: <= N nonzeros (z rows), else <= 2
+  T vec[NVMAX];   // a broadcast vector (Cholesky column, d, Householder v)
+  T vec2[NVMAX];
+  T npv[kWideNmax + 2];   // n_p: <= N nonzeros (z rows), else <= 2
   int npi[kWideNmax + 2];
   int npn;
   int nf;
   int p;
   int kd;
   int flag;
-  double best, bp, t1, sp, gc, gs;
+  T best, bp, t1, sp, gc, gs;
 };
 
-__device__ double block_sum(double x, Shared& sh) {
+template <typename T>
+__device__ T block_sum(T x, Shared<T>& sh) {
   x = wave_sum(x);
   __syncthreads();
   if ((threadIdx.x & 63) == 0) sh.red[threadIdx.x >> 6] = x;
   __syncthreads();
-  double s = 0.0;
+  T s = T(0);
 #pragma unroll
   for (int w = 0; w < WW; ++w) s += sh.red[w];
   return s;
 }
 
-__device__ void block_argmin(double& v, int& i, Shared& sh) {
+template <typename T>
+__device__ void block_argmin(T& v, int& i, Shared<T>& sh) {
   wave_argmin(v, i);
   __syncthreads();
   if ((threadIdx.x & 63) == 0) {
@@ -84,11 +87,12 @@ __device__ void block_argmin(double& v, int& i, Shared& sh) {
 
 // out[i] = sum_{k in [k0, n)} M[i*ld + k] vec[k] for rows i < n: one wave per
 // row, lanes over k (coalesced), then a wave reduction.
-__device__ void rows_dot(const double* M, int ld, int n, int k0, const double* vec, double* out) {
+template <typename T>
+__device__ void rows_dot(const T* M, int ld, int n, int k0, const T* vec, T* out) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   for (int i = w; i < n; i += WW) {
-    const double* row = M + (int64_t)i * ld;
-    double acc = 0.0;
+    const T* row = M + (int64_t)i * ld;
+    T acc = T(0);
     for (int k = k0 + lane; k < n; k += 64) acc = fma(row[k], vec[k], acc);
     acc = wave_sum(acc);
     if (lane == 0) out[i] = acc;
@@ -97,39 +101,42 @@ __device__ void rows_dot(const double* M, int ld, int n, int k0, const double* v
 
 __device__ __forceinline__ void gfence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup"); }
 
-template <int VAR>
-__device__ void wide_solve(const SolveArgs& a, const int N, const int64_t b, double* ws, Shared& sh) {
+template <int VAR, typename T>
+__device__ void wide_solve(const SolveArgs& a, const int N, const int64_t b, T* ws, Shared<T>& sh) {
   const WideLayout Lw(N);
   const int tid = threadIdx.x;
   const int NV = 6 * N;
-  const double dt = a.dt, dtm = dt / a.m;
-  double* xin = ws + Lw.XIN;
-  double* cc = ws + Lw.CC;
-  double* cs = ws + Lw.CS;
-  double* bw = ws + Lw.BW;
-  double* zb = ws + Lw.ZB;
-  double* xl = ws + Lw.XL;
-  double* xr = ws + Lw.XR;
-  double* pf = ws + Lw.PF;
-  double* ss = ws + Lw.SS;
-  double* dg = ws + Lw.DG;
-  double* aj = ws + Lw.AJ;
-  double* hv = ws + Lw.HV;
-  double* xv = ws + Lw.XV;
-  double* dv = ws + Lw.DV;
-  double* zv = ws + Lw.ZV;
-  double* wv = ws + Lw.WV;
-  double* uo = ws + Lw.UO;
-  double* rv = ws + Lw.RV;
-  double* ua = ws + Lw.UA;
+  const T dt = T(a.dt), dtm = dt / T(a.m);
+  T* xin = ws + Lw.XIN;
+  T* cc = ws + Lw.CC;
+  T* cs = ws + Lw.CS;
+  T* bw = ws + Lw.BW;
+  T* zb = ws + Lw.ZB;
+  T* xl = ws + Lw.XL;
+  T* xr = ws + Lw.XR;
+  T* pf = ws + Lw.PF;
+  T* ss = ws + Lw.SS;
+  T* dg = ws + Lw.DG;
+  T* aj = ws + Lw.AJ;
+  T* hv = ws + Lw.HV;
+  T* xv = ws + Lw.XV;
+  T* dv = ws + Lw.DV;
+  T* zv = ws + Lw.ZV;
+  T* wv = ws + Lw.WV;
+  T* uo = ws + Lw.UO;
+  T* rv = ws + Lw.RV;
+  T* ua = ws + Lw.UA;
   int* fr = reinterpret_cast<int*>(ws + Lw.FR);
   int* pos = reinterpret_cast<int*>(ws + Lw.POS);
   int* act = reinterpret_cast<int*>(ws + Lw.ACT);
   int* isa = reinterpret_cast<int*>(ws + Lw.ISA);
-  double* Rm = ws + Lw.RM;
-  double* H = ws + Lw.H;
-  double* J = ws + Lw.J;
+  T* Rm = ws + Lw.RM;
+  T* H = ws + Lw.H;
+  T* J = ws + Lw.J;
   const int ld = NV;   // row stride of H, J, R
+  // feasibility / degeneracy thresholds scaled to the arithmetic
+  const T tol = sizeof(T) == 4 ? T(1e-4) : T(kTol);
+  const T tiny = sizeof(T) == 4 ? T(1e-12) : T(1e-24);
 
   // ---------------- 0: inputs ------------------------------------------------
   {
@@ -143,7 +150,7 @@ __device__ void wide_solve(const SolveArgs& a, const int N, const int64_t b, dou
     const double* xp = a.x_lin + b * 12 * (N + 1);
     for (int i = tid; i < 12 * N; i += WT) {
       const int r = i / 12, c = i - 12 * r;
-      double v;
+      T v;
       if (a.shift_mode == 0) v = xp[i];
       else if (a.shift_mode == 1) v = r == 0 ? xin[c] : xr[i - 12];   // [x_in; x_ref] (3f :52-53)
       else v = r == 0 ? xin[c] : xp[(r + 1) * 12 + c];               // time shift (3f :59-62)
@@ -158,68 +165,68 @@ __device__ void wide_solve(const SolveArgs& a, const int N, const int64_t b, dou
   __syncthreads();
   // ---------------- 2: free response, S_t, adjoint (wave 0) -----------------
   if (tid < 64) {
-    double xrr = tid < 12 ? xin[tid] : 0.0;
-    const double qr = qdiag(tid);
-    double s[22];
+    T xrr = tid < 12 ? xin[tid] : T(0.0);
+    const T qr = T(qdiag(tid));
+    T s[22];
 #pragma unroll
     for (int a3 = 0; a3 < 3; ++a3) {
-      s[3 * a3] = kTermQ * kQ[a3];
-      s[3 * a3 + 1] = 0.0;
-      s[3 * a3 + 2] = kTermQ * kQ[6 + a3];
+      s[3 * a3] = T(kTermQ) * T(kQ[a3]);
+      s[3 * a3 + 1] = T(0.0);
+      s[3 * a3 + 2] = T(kTermQ) * T(kQ[6 + a3]);
     }
-    s[9] = kTermQ * kQ[5]; s[10] = 0.0; s[11] = kTermQ * kQ[11];
-    s[12] = kTermQ * kQ[3]; s[13] = 0.0; s[14] = kTermQ * kQ[4];
-    s[15] = s[16] = s[17] = s[18] = 0.0;
-    s[19] = kTermQ * kQ[9]; s[20] = 0.0; s[21] = kTermQ * kQ[10];
+    s[9] = T(kTermQ) * T(kQ[5]); s[10] = T(0.0); s[11] = T(kTermQ) * T(kQ[11]);
+    s[12] = T(kTermQ) * T(kQ[3]); s[13] = T(0.0); s[14] = T(kTermQ) * T(kQ[4]);
+    s[15] = s[16] = s[17] = s[18] = T(0.0);
+    s[19] = T(kTermQ) * T(kQ[9]); s[20] = T(0.0); s[21] = T(kTermQ) * T(kQ[10]);
     if (tid == 2) zb[0] = xrr;
     if (tid == 0)
       for (int e = 0; e < 22; ++e) ss[22 * (N - 1) + e] = s[e];
     for (int k = 0; k < N; ++k) {
-      const double cp = cs[2 * k], sp = cs[2 * k + 1];
-      xrr = ad_lane(xrr, dt, cp, sp) + ((tid == 8) ? -a.g * dt : 0.0);
-      const double kf = (k == N - 1) ? kTermQ : 1.0;
+      const T cp = cs[2 * k], sp = cs[2 * k + 1];
+      xrr = ad_lane(xrr, dt, cp, sp) + ((tid == 8) ? -T(a.g) * dt : T(0.0));
+      const T kf = (k == N - 1) ? T(kTermQ) : T(1.0);
       if (tid < 12) dg[12 * k + tid] = kf * qr * (xrr - xr[12 * k + tid]);
       if (tid == 2) zb[k + 1] = xrr;
       const int t = N - 1 - k;
       if (t >= 1) {
-        const double ct = cs[2 * t], st = cs[2 * t + 1];
+        const T ct = cs[2 * t], st = cs[2 * t + 1];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int o = 3 * q;
-          const double aa = s[o], bb = s[o + 1], cc2 = s[o + 2];
+          const T aa = s[o], bb = s[o + 1], cc2 = s[o + 2];
           s[o + 1] = fma(dt, aa, bb);
-          s[o + 2] = cc2 + dt * (2.0 * bb + dt * aa);
+          s[o + 2] = cc2 + dt * (T(2.0) * bb + dt * aa);
         }
-        const double D00 = ct * dt, D01 = st * dt, D10 = -st * dt, D11 = ct * dt;
-        const double P00 = s[12], P01 = s[13], P11 = s[14];
-        const double M00 = s[15], M01 = s[16], M10 = s[17], M11 = s[18];
-        const double N00 = M00 + (P00 * D00 + P01 * D10), N01 = M01 + (P00 * D01 + P01 * D11);
-        const double N10 = M10 + (P01 * D00 + P11 * D10), N11 = M11 + (P01 * D01 + P11 * D11);
-        const double A00 = D00 * N00 + D10 * N10, A01 = D00 * N01 + D10 * N11;
-        const double A11 = D01 * N01 + D11 * N11;
-        const double B00 = M00 * D00 + M10 * D10, B01 = M00 * D01 + M10 * D11;
-        const double B11 = M01 * D01 + M11 * D11;
+        const T D00 = ct * dt, D01 = st * dt, D10 = -st * dt, D11 = ct * dt;
+        const T P00 = s[12], P01 = s[13], P11 = s[14];
+        const T M00 = s[15], M01 = s[16], M10 = s[17], M11 = s[18];
+        const T N00 = M00 + (P00 * D00 + P01 * D10), N01 = M01 + (P00 * D01 + P01 * D11);
+        const T N10 = M10 + (P01 * D00 + P11 * D10), N11 = M11 + (P01 * D01 + P11 * D11);
+        const T A00 = D00 * N00 + D10 * N10, A01 = D00 * N01 + D10 * N11;
+        const T A11 = D01 * N01 + D11 * N11;
+        const T B00 = M00 * D00 + M10 * D10, B01 = M00 * D01 + M10 * D11;
+        const T B11 = M01 * D01 + M11 * D11;
         s[19] += A00 + B00;
         s[20] += A01 + B01;
         s[21] += A11 + B11;
         s[15] = N00; s[16] = N01; s[17] = N10; s[18] = N11;
 #pragma unroll
         for (int a3 = 0; a3 < 3; ++a3) {
-          s[3 * a3] += kQ[a3];
-          s[3 * a3 + 2] += kQ[6 + a3];
+          s[3 * a3] += T(kQ[a3]);
+          s[3 * a3 + 2] += T(kQ[6 + a3]);
         }
-        s[9] += kQ[5]; s[11] += kQ[11];
-        s[12] += kQ[3]; s[14] += kQ[4];
-        s[19] += kQ[9]; s[21] += kQ[10];
+        s[9] += T(kQ[5]); s[11] += T(kQ[11]);
+        s[12] += T(kQ[3]); s[14] += T(kQ[4]);
+        s[19] += T(kQ[9]); s[21] += T(kQ[10]);
         if (tid == 0)
           for (int e = 0; e < 22; ++e) ss[22 * (t - 1) + e] = s[e];
       }
     }
     gfence();
-    double ar = tid < 12 ? dg[12 * (N - 1) + tid] : 0.0;
+    T ar = tid < 12 ? dg[12 * (N - 1) + tid] : T(0.0);
     if (tid >= 6 && tid < 12) aj[6 * (N - 1) + tid - 6] = ar;
     for (int t = N - 1; t >= 1; --t) {
-      ar = adt_lane(ar, dt, cs[2 * t], cs[2 * t + 1]) + (tid < 12 ? dg[12 * (t - 1) + tid] : 0.0);
+      ar = adt_lane(ar, dt, cs[2 * t], cs[2 * t + 1]) + (tid < 12 ? dg[12 * (t - 1) + tid] : T(0.0));
       if (tid >= 6 && tid < 12) aj[6 * (t - 1) + tid - 6] = ar;
     }
   }
@@ -228,7 +235,7 @@ __device__ void wide_solve(const SolveArgs& a, const int N, const int64_t b, dou
     int nf = 0;
     for (int v = 0; v < NV; ++v) {
       const int k = v / 6, c = v - 6 * k;
-      const bool fixed = (c < 3 && cc[k] == 0.0) || (VAR == 2 && c == 1);   // :134-136, 2f :129
+      const bool fixed = (c < 3 && cc[k] == T(0.0)) || (VAR == 2 && c == 1);   // :134-136, 2f :129
       pos[v] = fixed ? -1 : nf;
       if (!fixed) fr[nf++] = v;
     }
@@ -237,40 +244,40 @@ __device__ void wide_solve(const SolveArgs& a, const int N, const int64_t b, dou
   gfence();
   __syncthreads();
   const int NF = sh.nf;
-  const double ubar_alias = (cc[N - 1] != 0.0) ? 2.0 * a.m * a.g : 0.0;
+  const T ubar_alias = (cc[N - 1] != T(0.0)) ? T(2.0) * T(a.m) * T(a.g) : T(0.0);
   for (int r = tid; r < NF; r += WT) {
     const int v = fr[r];
     const int ii = v / 6, ci = v - 6 * ii;
-    const double cpi = cs[2 * ii], spi = cs[2 * ii + 1];
-    const double* bwi = bw + 18 * ii;
-    double e0[12], f[12], g[12];
-    for (int q = 0; q < 6; ++q) e0[q] = 0.0;
-    for (int q = 0; q < 3; ++q) e0[6 + q] = ci < 3 ? bv<VAR>(q, ci, dtm, cpi, spi) : 0.0;
+    const T cpi = cs[2 * ii], spi = cs[2 * ii + 1];
+    const T* bwi = bw + 18 * ii;
+    T e0[12], f[12], g[12];
+    for (int q = 0; q < 6; ++q) e0[q] = T(0.0);
+    for (int q = 0; q < 3; ++q) e0[6 + q] = ci < 3 ? bv<VAR>(q, ci, dtm, cpi, spi) : T(0.0);
     for (int q = 0; q < 3; ++q) e0[9 + q] = bwi[6 * q + ci];
     s_times(ss + 22 * ii, e0, f);
-    double* Hr = H + (int64_t)r * ld;
+    T* Hr = H + (int64_t)r * ld;
     for (int c2 = 0; c2 <= ci; ++c2) {   // diagonal block, columns <= mine
       const int pw = pos[6 * ii + c2];
       if (pw < 0) continue;
-      double hd = bd_dot<VAR>(c2, f, bwi, dtm, cpi, spi);
-      if (c2 == ci && ii != N - 1) hd += 2.0 * kRdiag;
+      T hd = bd_dot<VAR>(c2, f, bwi, dtm, cpi, spi);
+      if (c2 == ci && ii != N - 1) hd += T(2.0) * T(kRdiag);
       Hr[pw] = hd;
     }
-    double hacc = 0.0;
+    T hacc = T(0.0);
     for (int q = 0; q < 6; ++q) hacc = fma(e0[6 + q], aj[6 * ii + q], hacc);
     for (int q = 0; q < 12; ++q) g[q] = f[q];
     for (int j = ii - 1; j >= 0; --j) {
       adt_times(g, dt, cs[2 * (j + 1)], cs[2 * (j + 1) + 1]);
-      const double cp = cs[2 * j], sp = cs[2 * j + 1];
+      const T cp = cs[2 * j], sp = cs[2 * j + 1];
       for (int c2 = 0; c2 < 6; ++c2) {
         const int pw = pos[6 * j + c2];
         if (pw >= 0) Hr[pw] = bd_dot<VAR>(c2, g, bw + 18 * j, dtm, cp, sp);
       }
     }
-    double ub = 0.0;
-    if (ci == 2) ub = a.uref_aliased ? ubar_alias : ((cc[ii] != 0.0) ? 2.0 * a.m * a.g : 0.0);
-    const double Vj = (ii == N - 1) ? 0.0 : kRdiag;
-    hv[r] = 2.0 * hacc - 2.0 * Vj * ub;
+    T ub = T(0.0);
+    if (ci == 2) ub = a.uref_aliased ? ubar_alias : ((cc[ii] != T(0.0)) ? T(2.0) * T(a.m) * T(a.g) : T(0.0));
+    const T Vj = (ii == N - 1) ? T(0.0) : T(kRdiag);
+    hv[r] = T(2.0) * hacc - T(2.0) * Vj * ub;
   }
   gfence();
   __syncthreads();
@@ -278,11 +285,11 @@ __device__ void wide_solve(const SolveArgs& a, const int N, const int64_t b, dou
   int status = ST_SOLVED;
   // ---------------- 4: Cholesky --------------------------------------------
   for (int k = 0; k < NF; ++k) {
-    const double piv = H[(int64_t)k * ld + k];
-    if (!(piv > 0.0)) { status = ST_NUMERICAL; break; }
-    const double lkk = sqrt(piv), rl = 1.0 / lkk;
+    const T piv = H[(int64_t)k * ld + k];
+    if (!(piv > T(0.0))) { status = ST_NUMERICAL; break; }
+    const T lkk = sqrt(piv), rl = T(1.0) / lkk;
     for (int i = k + 1 + tid; i < NF; i += WT) {
-      const double l = H[(int64_t)i * ld + k] * rl;
+      const T l = H[(int64_t)i * ld + k] * rl;
       H[(int64_t)i * ld + k] = l;
       sh.vec[i] = l;
     }
@@ -290,8 +297,8 @@ __device__ void wide_solve(const SolveArgs& a, const int N, const int64_t b, dou
     __syncthreads();   // every thread has read the pivot; column k published
     if (tid == 0) H[(int64_t)k * ld + k] = lkk;
     for (int i = k + 1; i < NF; ++i) {
-      const double li = sh.vec[i];
-      double* Hi = H + (int64_t)i * ld;
+      const T li = sh.vec[i];
+      T* Hi = H + (int64_t)i * ld;
       for (int j = k + 1 + tid; j <= i; j += WT) Hi[j] = fma(-li, sh.vec[j], Hi[j]);
     }
     gfence();
@@ -300,11 +307,11 @@ __device__ void wide_solve(const SolveArgs& a, const int N, const int64_t b, dou
   // ---------------- 5: J = L^-T (row c of J = column c of L^-1) -------------
   if (status == ST_SOLVED) {
     for (int c = tid; c < NF; c += WT) {
-      double* Jc = J + (int64_t)c * ld;
-      for (int i = 0; i < c; ++i) Jc[i] = 0.0;
+      T* Jc = J + (int64_t)c * ld;
+      for (int i = 0; i < c; ++i) Jc[i] = T(0.0);
       for (int i = c; i < NF; ++i) {
-        const double* Li = H + (int64_t)i * ld;
-        double acc = (i == c) ? 1.0 : 0.0;
+        const T* Li = H + (int64_t)i * ld;
+        T acc = (i == c) ? T(1.0) : T(0.0);
         for (int k = c; k < i; ++k) acc = fma(-Li[k], Jc[k], acc);
         Jc[i] = acc / Li[i];
       }
@@ -314,13 +321,13 @@ __device__ void wide_solve(const SolveArgs& a, const int N, const int64_t b, dou
   }
   // ---------------- 6: Goldfarb-Idnani -------------------------------------
   int iters = 0;
-  const double mu = a.mu ? a.mu[b] : a.mu_default;
-  const double zc = dt * dtm;   // coefficient scale of fz_j in z_k (Bd[8][2] = dt/m)
-  if (xin[2] - kZmin < -kTol || zb[1] - kZmin < -kTol) status = ST_INFEAS;   // constant rows z_0, z_1
+  const T mu = T(a.mu ? a.mu[b] : a.mu_default);
+  const T zc = dt * dtm;   // coefficient scale of fz_j in z_k (Bd[8][2] = dt/m)
+  if (xin[2] - T(kZmin) < -tol || zb[1] - T(kZmin) < -tol) status = ST_INFEAS;   // constant rows z_0, z_1
   if (status == ST_SOLVED) {
     // x = -J J' h
     for (int i = tid; i < NF; i += WT) {
-      double acc = 0.0;
+      T acc = T(0.0);
       for (int k = 0; k <= i; ++k) acc = fma(J[(int64_t)k * ld + i], hv[k], acc);
       sh.vec[i] = acc;
     }
@@ -338,35 +345,35 @@ __device__ void wide_solve(const SolveArgs& a, const int N, const int64_t b, dou
   bool done = status != ST_SOLVED;
   while (!done) {
     // ---- slacks of every constraint; the most violated one ----
-    double best = INFINITY;
+    T best = INFINITY;
     int bid = 0x7fffffff;
     for (int v = tid; v < NV; v += WT) {
       const int j = v / 6, c = v - 6 * j;
-      const bool stance = cc[j] != 0.0;
-      const double xvv = pos[v] >= 0 ? xv[pos[v]] : 0.0;
-      double s0 = INFINITY, s1 = INFINITY, s2 = INFINITY;
+      const bool stance = cc[j] != T(0.0);
+      const T xvv = pos[v] >= 0 ? xv[pos[v]] : T(0.0);
+      T s0 = INFINITY, s1 = INFINITY, s2 = INFINITY;
       if (c >= 3) {
-        const double lim = tau_lim(c);
+        const T lim = T(tau_lim(c));
         s0 = xvv + lim;
         s1 = lim - xvv;
         if (c == 3 && j >= 2) {
-          double z1 = 0.0, n2 = 0.0;
+          T z1 = T(0.0), n2 = T(0.0);
           for (int jj = 0; jj <= j - 2; ++jj) {
-            if (cc[jj] == 0.0) continue;
-            const double cz = zc * (double)(j - 1 - jj);
+            if (cc[jj] == T(0.0)) continue;
+            const T cz = zc * (T)(j - 1 - jj);
             z1 = fma(cz, xv[pos[6 * jj + 2]], z1);
             n2 = fma(cz, cz, n2);
           }
-          const double zrow = (zb[j] - kZmin) + z1;
-          s2 = n2 > 0.0 ? zrow / sqrt(n2) : ((zrow < -kTol) ? -INFINITY : INFINITY);
+          const T zrow = (zb[j] - T(kZmin)) + z1;
+          s2 = n2 > T(0.0) ? zrow / sqrt(n2) : ((zrow < -tol) ? -INFINITY : INFINITY);
         }
       } else if (stance && !(VAR == 2 && c == 1)) {
-        const double fz = xv[pos[6 * j + 2]];
+        const T fz = xv[pos[6 * j + 2]];
         if (c == 2) {
           s0 = fz;
-          s1 = kFzMax - fz;
+          s1 = T(kFzMax) - fz;
         } else {
-          const double inv = 1.0 / sqrt(1.0 + mu * mu);
+          const T inv = T(1.0) / sqrt(T(1.0) + mu * mu);
           s0 = (mu * fz - xvv) * inv;
           s1 = (mu * fz + xvv) * inv;
         }
@@ -376,27 +383,27 @@ __device__ void wide_solve(const SolveArgs& a, const int N, const int64_t b, dou
       if (!isa[4 * v + 2]) argmin_combine(best, bid, s2, 4 * v + 2);
     }
     block_argmin(best, bid, sh);
-    if (!(best < -kTol)) break;   // primal feasible: optimal
+    if (!(best < -tol)) break;   // primal feasible: optimal
     const int p = bid;
     // n_p as (free index, coefficient) pairs and its rhs b_p
     if (tid == 0) {
       const int v = p >> 2, sl = p & 3, j = v / 6, c = v - 6 * j;
       int n = 0;
-      double bp = 0.0;
+      T bp = T(0.0);
       if (c >= 3) {
         if (sl < 2) {
-          sh.npi[n] = pos[v]; sh.npv[n++] = sl == 0 ? 1.0 : -1.0;
-          bp = -tau_lim(c);
+          sh.npi[n] = pos[v]; sh.npv[n++] = sl == 0 ? T(1.0) : -T(1.0);
+          bp = -T(tau_lim(c));
         } else {
           for (int jj = 0; jj <= j - 2; ++jj)
-            if (cc[jj] != 0.0) { sh.npi[n] = pos[6 * jj + 2]; sh.npv[n++] = zc * (double)(j - 1 - jj); }
-          bp = kZmin - zb[j];
+            if (cc[jj] != T(0.0)) { sh.npi[n] = pos[6 * jj + 2]; sh.npv[n++] = zc * (T)(j - 1 - jj); }
+          bp = T(kZmin) - zb[j];
         }
       } else if (c == 2) {
-        sh.npi[n] = pos[v]; sh.npv[n++] = sl == 0 ? 1.0 : -1.0;
-        bp = sl == 0 ? 0.0 : -kFzMax;
+        sh.npi[n] = pos[v]; sh.npv[n++] = sl == 0 ? T(1.0) : -T(1.0);
+        bp = sl == 0 ? T(0.0) : -T(kFzMax);
       } else {
-        sh.npi[n] = pos[v]; sh.npv[n++] = sl == 0 ? -1.0 : 1.0;
+        sh.npi[n] = pos[v]; sh.npv[n++] = sl == 0 ? -T(1.0) : T(1.0);
         sh.npi[n] = pos[6 * j + 2]; sh.npv[n++] = mu;
       }
       sh.npn = n;
@@ -404,13 +411,13 @@ __device__ void wide_solve(const SolveArgs& a, const int N, const int64_t b, dou
     }
     __syncthreads();
     const int npn = sh.npn;
-    const double bp = sh.bp;
-    double uplus = 0.0;
+    const T bp = sh.bp;
+    T uplus = T(0.0);
     while (true) {
       if (++iters > max_iter) { status = ST_MAXIT; done = true; break; }
       // d = J' n_p (a combination of <= N rows of J)
       for (int i = tid; i < NF; i += WT) {
-        double acc = 0.0;
+        T acc = T(0.0);
         for (int e = 0; e < npn; ++e) acc = fma(sh.npv[e], J[(int64_t)sh.npi[e] * ld + i], acc);
         sh.vec[i] = acc;
         dv[i] = acc;
@@ -418,9 +425,9 @@ __device__ void wide_solve(const SolveArgs& a, const int N, const int64_t b, dou
       __syncthreads();
       // z = J2 d2, |d2|^2, |d|^2
       rows_dot(J, ld, NF, q, sh.vec, zv);
-      double zz = 0.0, dd = 0.0;
+      T zz = T(0.0), dd = T(0.0);
       for (int i = tid; i < NF; i += WT) {
-        const double di = sh.vec[i];
+        const T di = sh.vec[i];
         dd = fma(di, di, dd);
         if (i >= q) zz = fma(di, di, zz);
       }
@@ -431,15 +438,15 @@ __device__ void wide_solve(const SolveArgs& a, const int N, const int64_t b, dou
       // r = R^-1 d1, the drop candidate and n_p' x - b_p (q, n_p small: one thread)
       if (tid == 0) {
         for (int i = q - 1; i >= 0; --i) {
-          double t = sh.vec[i];
+          T t = sh.vec[i];
           for (int k = i + 1; k < q; ++k) t = fma(-Rm[(int64_t)i * ld + k], rv[k], t);
           rv[i] = t / Rm[(int64_t)i * ld + i];
         }
-        double t1 = INFINITY;
+        T t1 = INFINITY;
         int kd = -1;
         for (int j = 0; j < q; ++j)
-          if (rv[j] > 0.0 && ua[j] / rv[j] < t1) { t1 = ua[j] / rv[j]; kd = j; }
-        double sp = -bp;
+          if (rv[j] > T(0.0) && ua[j] / rv[j] < t1) { t1 = ua[j] / rv[j]; kd = j; }
+        T sp = -bp;
         for (int e = 0; e < npn; ++e) sp = fma(sh.npv[e], xv[sh.npi[e]], sp);
         sh.t1 = t1;
         sh.kd = kd;
@@ -447,11 +454,11 @@ __device__ void wide_solve(const SolveArgs& a, const int N, const int64_t b, dou
       }
       gfence();
       __syncthreads();
-      const double t1 = sh.t1, sp = sh.sp;
+      const T t1 = sh.t1, sp = sh.sp;
       const int kd = sh.kd;
-      const bool has_z = zz > 1e-24 * dd;
-      const double t2 = has_z ? -sp / zz : INFINITY;   // n_p' z = |d2|^2
-      const double t = t1 < t2 ? t1 : t2;
+      const bool has_z = zz > tiny * dd;
+      const T t2 = has_z ? -sp / zz : INFINITY;   // n_p' z = |d2|^2
+      const T t = t1 < t2 ? t1 : t2;
       if (!(t < INFINITY)) { status = ST_INFEAS; done = true; break; }
       if (has_z)
         for (int i = tid; i < NF; i += WT) xv[i] = fma(t, zv[i], xv[i]);
@@ -462,10 +469,10 @@ __device__ void wide_solve(const SolveArgs& a, const int N, const int64_t b, dou
       __syncthreads();
       if (has_z && t == t2) {
         // ---- add p: one Householder reflection maps d2 onto alpha e_q ----
-        const double dq = sh.vec[q];
-        const double alpha = sqrt(zz);
-        const double sg = dq >= 0.0 ? 1.0 : -1.0;
-        const double beta = 1.0 / (alpha * (alpha + fabs(dq)));   // 2 / v'v
+        const T dq = sh.vec[q];
+        const T alpha = sqrt(zz);
+        const T sg = dq >= T(0.0) ? T(1.0) : -T(1.0);
+        const T beta = T(1.0) / (alpha * (alpha + fabs(dq)));   // 2 / v'v
         for (int k = q + tid; k < NF; k += WT) sh.vec2[k] = (k == q) ? dq + sg * alpha : sh.vec[k];
         __syncthreads();
         rows_dot(J, ld, NF, q, sh.vec2, wv);   // w = J2 v
@@ -474,11 +481,11 @@ __device__ void wide_solve(const SolveArgs& a, const int N, const int64_t b, dou
         // J2 <- J2 (I - beta v v'); column q flips sign when sg > 0 so that
         // the new R diagonal is +alpha
         for (int i = 0; i < NF; ++i) {
-          double* Ji = J + (int64_t)i * ld;
-          const double bwi = beta * wv[i];
+          T* Ji = J + (int64_t)i * ld;
+          const T bwi = beta * wv[i];
           for (int k = q + tid; k < NF; k += WT) {
-            double x = fma(-bwi, sh.vec2[k], Ji[k]);
-            if (k == q && sg > 0.0) x = -x;
+            T x = fma(-bwi, sh.vec2[k], Ji[k]);
+            if (k == q && sg > T(0.0)) x = -x;
             Ji[k] = x;
           }
         }
@@ -507,12 +514,12 @@ __device__ void wide_solve(const SolveArgs& a, const int N, const int64_t b, dou
       __syncthreads();
       for (int j = kd; j < q - 1; ++j) {
         if (tid == 0) {
-          const double aa = Rm[(int64_t)j * ld + j], bb = Rm[(int64_t)(j + 1) * ld + j];
-          const double hh = sqrt(aa * aa + bb * bb);
-          double c = 1.0, s = 0.0;
-          if (hh != 0.0) { c = aa / hh; s = bb / hh; }
+          const T aa = Rm[(int64_t)j * ld + j], bb = Rm[(int64_t)(j + 1) * ld + j];
+          const T hh = sqrt(aa * aa + bb * bb);
+          T c = T(1.0), s = T(0.0);
+          if (hh != T(0.0)) { c = aa / hh; s = bb / hh; }
           for (int k = j; k < q - 1; ++k) {
-            const double r0 = Rm[(int64_t)j * ld + k], r1 = Rm[(int64_t)(j + 1) * ld + k];
+            const T r0 = Rm[(int64_t)j * ld + k], r1 = Rm[(int64_t)(j + 1) * ld + k];
             Rm[(int64_t)j * ld + k] = c * r0 + s * r1;
             Rm[(int64_t)(j + 1) * ld + k] = -s * r0 + c * r1;
           }
@@ -521,10 +528,10 @@ __device__ void wide_solve(const SolveArgs& a, const int N, const int64_t b, dou
         }
         gfence();
         __syncthreads();
-        const double c = sh.gc, s = sh.gs;
+        const T c = sh.gc, s = sh.gs;
         for (int i = tid; i < NF; i += WT) {
-          double* Ji = J + (int64_t)i * ld;
-          const double x0 = Ji[j], x1 = Ji[j + 1];
+          T* Ji = J + (int64_t)i * ld;
+          const T x0 = Ji[j], x1 = Ji[j + 1];
           Ji[j] = c * x0 + s * x1;
           Ji[j + 1] = -s * x0 + c * x1;
         }
@@ -532,7 +539,7 @@ __device__ void wide_solve(const SolveArgs& a, const int N, const int64_t b, dou
         __syncthreads();
       }
       if (tid == 0)
-        for (int i = 0; i < q; ++i) Rm[(int64_t)i * ld + q - 1] = 0.0;
+        for (int i = 0; i < q; ++i) Rm[(int64_t)i * ld + q - 1] = T(0.0);
       --q;
       gfence();
       __syncthreads();
@@ -540,7 +547,7 @@ __device__ void wide_solve(const SolveArgs& a, const int N, const int64_t b, dou
   }
   // ---------------- 7: outputs ---------------------------------------------
   for (int v = tid; v < NV; v += WT) {
-    const double u = (status == ST_SOLVED && pos[v] >= 0) ? xv[pos[v]] : 0.0;
+    const T u = (status == ST_SOLVED && pos[v] >= 0) ? xv[pos[v]] : T(0.0);
     uo[v] = u;
     a.u[b * NV + v] = u;
   }
@@ -548,39 +555,39 @@ __device__ void wide_solve(const SolveArgs& a, const int N, const int64_t b, dou
   __syncthreads();
   double* xo = a.x ? a.x + b * 12 * (N + 1) : nullptr;
   if (tid < 64) {
-    double xrr = tid < 12 ? xin[tid] : 0.0;
+    T xrr = tid < 12 ? xin[tid] : T(0.0);
     if (xo && tid < 12) xo[tid] = xrr;
-    const double qr = qdiag(tid);
+    const T qr = T(qdiag(tid));
     const int rw = (tid >= 9 && tid < 12) ? tid - 9 : 0;
     const int rvv = (tid >= 6 && tid < 9) ? tid - 6 : 0;
-    double objl = 0.0;
+    T objl = T(0.0);
     for (int k = 0; k < N; ++k) {
-      const double cp = cs[2 * k], sp = cs[2 * k + 1];
-      const double* bwr = bw + 18 * k + 6 * rw;
-      const double* uk = uo + 6 * k;
-      double bw_u = 0.0;
+      const T cp = cs[2 * k], sp = cs[2 * k + 1];
+      const T* bwr = bw + 18 * k + 6 * rw;
+      const T* uk = uo + 6 * k;
+      T bw_u = T(0.0);
       for (int c = 0; c < 6; ++c) bw_u = fma(bwr[c], uk[c], bw_u);
-      double bv_u;
+      T bv_u;
       if constexpr (VAR == 3) {
         bv_u = dtm * uk[rvv];
       } else {   // Rz' dt/m
-        const double u0 = uk[0], u1 = uk[1], u2 = uk[2];
+        const T u0 = uk[0], u1 = uk[1], u2 = uk[2];
         bv_u = (rvv == 0) ? dtm * (cp * u0 - sp * u1) : ((rvv == 1) ? dtm * (sp * u0 + cp * u1) : dtm * u2);
       }
-      const double bu = (tid >= 9 && tid < 12) ? bw_u : ((tid >= 6 && tid < 9) ? bv_u : 0.0);
-      xrr = ad_lane(xrr, dt, cp, sp) + bu + ((tid == 8) ? -a.g * dt : 0.0);
-      const double kf = (k == N - 1) ? kTermQ : 1.0;
-      const double e = xrr - (tid < 12 ? xr[12 * k + tid] : 0.0);
+      const T bu = (tid >= 9 && tid < 12) ? bw_u : ((tid >= 6 && tid < 9) ? bv_u : T(0.0));
+      xrr = ad_lane(xrr, dt, cp, sp) + bu + ((tid == 8) ? -T(a.g) * dt : T(0.0));
+      const T kf = (k == N - 1) ? T(kTermQ) : T(1.0);
+      const T e = xrr - (tid < 12 ? xr[12 * k + tid] : T(0.0));
       objl = fma(kf * qr * e, e, objl);
       if (k < N - 1 && tid < 6) {
-        const double ubz = a.uref_aliased ? ((cc[N - 1] != 0.0) ? 2.0 * a.m * a.g : 0.0)
-                                          : ((cc[k] != 0.0) ? 2.0 * a.m * a.g : 0.0);
-        const double du = uk[tid] - (tid == 2 ? ubz : 0.0);
+        const T ubz = a.uref_aliased ? ((cc[N - 1] != T(0.0)) ? T(2.0) * T(a.m) * T(a.g) : T(0.0))
+                                          : ((cc[k] != T(0.0)) ? T(2.0) * T(a.m) * T(a.g) : T(0.0));
+        const T du = uk[tid] - (tid == 2 ? ubz : T(0.0));
         objl = fma(kRdiag * du, du, objl);
       }
       if (xo && tid < 12) xo[12 * (k + 1) + tid] = xrr;
     }
-    const double objv = wave_sum(objl);
+    const T objv = wave_sum(objl);
     if (tid == 0) {
       if (a.obj) a.obj[b] = objv;
       a.status[b] = status;
@@ -589,12 +596,12 @@ __device__ void wide_solve(const SolveArgs& a, const int N, const int64_t b, dou
   }
 }
 
-template <int VAR>
+template <int VAR, typename T>
 __global__ void __launch_bounds__(WT, 2) wide_kernel(SolveArgs a, int N) {
-  __shared__ Shared sh;
-  double* ws = a.ws + (int64_t)blockIdx.x * a.ws_stride;
+  __shared__ Shared<T> sh;
+  T* ws = reinterpret_cast<T*>(a.ws) + (int64_t)blockIdx.x * a.ws_stride;
   for (int64_t b = blockIdx.x; b < a.B; b += gridDim.x) {
-    wide_solve<VAR>(a, N, b, ws, sh);
+    wide_solve<VAR, T>(a, N, b, ws, sh);
     gfence();
     __syncthreads();
   }
@@ -606,12 +613,15 @@ bool launch_solve_wide(int variant, int N, const SolveArgs& a, hipStream_t s) {
   if (N < 1 || N > kWideNmax || !a.ws || a.ws_groups < 1) return false;
   if (a.B <= 0) return true;
   const int64_t g = a.B < a.ws_groups ? a.B : a.ws_groups;
+  const bool f32 = a.precision == 1;
   if (variant == 3) {
-    hipLaunchKernelGGL((wide_kernel<3>), dim3((unsigned)g), dim3(WT), 0, s, a, N);
+    if (f32) hipLaunchKernelGGL((wide_kernel<3, float>), dim3((unsigned)g), dim3(WT), 0, s, a, N);
+    else hipLaunchKernelGGL((wide_kernel<3, double>), dim3((unsigned)g), dim3(WT), 0, s, a, N);
     return true;
   }
   if (variant == 2) {
-    hipLaunchKernelGGL((wide_kernel<2>), dim3((unsigned)g), dim3(WT), 0, s, a, N);
+    if (f32) hipLaunchKernelGGL((wide_kernel<2, float>), dim3((unsigned)g), dim3(WT), 0, s, a, N);
+    else hipLaunchKernelGGL((wide_kernel<2, double>), dim3((unsigned)g), dim3(WT), 0, s, a, N);
     return true;
   }
   return false;

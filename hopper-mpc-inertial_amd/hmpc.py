@@ -21,6 +21,7 @@ ERRORS = {-1: 'HMPC_ERR_ARG', -2: 'HMPC_ERR_UNSUPPORTED', -3: 'HMPC_ERR_HIP', -4
 STATUS = {0: 'solved', 1: 'max_iter', 2: 'primal_infeasible', 3: 'numerical'}
 VARIANTS = {'3f': 3, '2f': 2, 3: 3, 2: 2}
 UREF = {'aliased': 0, 'per_stage': 1}
+PRECISION = {'f64': 0, 'f32': 1, 'f64_generic': 2}
 
 # symbol -> (restype, argtypes); every symbol declared in include/hmpc.h
 _D = ctypes.POINTER(ctypes.c_double)
@@ -44,6 +45,7 @@ SIGNATURES = {
                                         _VP, ctypes.c_int64, _VP, ctypes.c_int64, ctypes.c_int64,
                                         _VP, _VP, _VP]),
     'hmpc_convert_batch': (ctypes.c_int, [_VP, ctypes.c_int64, _VP, _VP, _VP]),
+    'hmpc_set_precision': (ctypes.c_int, [_VP, ctypes.c_int]),
     'hmpc_last_error': (ctypes.c_char_p, [_VP]),
     'hmpc_time_solve_batch': (ctypes.c_int, [_VP, ctypes.c_int64] + [_VP] * 11
                               + [ctypes.c_int, _VP, ctypes.POINTER(ctypes.c_double)]),
@@ -95,7 +97,7 @@ class Context:
     (variant, N) and the Runner's physical constants."""
 
     def __init__(self, variant='3f', N=10, t=0.02, m=7.5, g=9.807, mu=1.0, Jinv=None, rh=None,
-                 uref_mode='aliased', device=0):
+                 uref_mode='aliased', device=0, precision='f64'):
         lib = load()
         if Jinv is None or rh is None:
             raise ValueError('Jinv and rh are required')
@@ -112,6 +114,8 @@ class Context:
             raise HmpcError(f'hmpc_create({variant}, N={N}) failed: {ERRORS.get(rc, rc)}')
         self._h = h
         self._lib = lib
+        if precision != 'f64':
+            self._check(lib.hmpc_set_precision(h, PRECISION[precision]), 'hmpc_set_precision')
 
     def close(self):
         if getattr(self, '_h', None):

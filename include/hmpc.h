@@ -65,6 +65,12 @@ extern "C" {
                                      the last stage's u_ref (the default)        */
 #define HMPC_UREF_PER_STAGE 1     /* the intended per-stage 2mg*C[k]             */
 
+/* arithmetic of the solve (hmpc_set_precision) */
+#define HMPC_PREC_F64 0           /* fp64; the dedicated kernel when N has one (default) */
+#define HMPC_PREC_F32 1           /* fp32 arithmetic (generic kernel; BASELINE configs[4]:
+                                     the tolerance/throughput trade-off)          */
+#define HMPC_PREC_F64_GENERIC 2   /* fp64 on the generic kernel (its fp32 twin's A/B) */
+
 typedef struct hmpc_ctx hmpc_ctx;
 
 /* ABI version (major*10000 + minor*100 + patch) */
@@ -155,6 +161,12 @@ int hmpc_plant_batch(hmpc_ctx* ctx, int64_t B, int n_steps, double dt, const dou
 
 /* x [B,12] = convert(X [B,13]) (src/robotrunner.py:19-28).  Asynchronous. */
 int hmpc_convert_batch(hmpc_ctx* ctx, int64_t B, const double* X, double* x, void* stream);
+
+/* Arithmetic of every later solve on this context (HMPC_PREC_*; inputs and
+   outputs stay fp64 at the ABI).  BASELINE configs[4] asks for fp32 vs fp64:
+   fp32 loses most of the 1e-6 tolerance on this ill-conditioned problem
+   (reduced Hessian condition ~3e6), see DESIGN.md. */
+int hmpc_set_precision(hmpc_ctx* ctx, int precision);
 
 /* Last HIP error string of this context ("" if none). */
 const char* hmpc_last_error(hmpc_ctx* ctx);
