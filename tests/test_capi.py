@@ -47,8 +47,10 @@ def test_argument_errors_do_not_need_a_gpu():
     r = (ctypes.c_double * 3)(0, 0, 0)
     assert lib.hmpc_create(ctypes.byref(h), 7, 10, 0.02, 7.5, 9.807, 1.0, J, r, 0, 0) == -1
     assert lib.hmpc_create(ctypes.byref(h), 3, 10, -1.0, 7.5, 9.807, 1.0, J, r, 0, 0) == -1
-    assert lib.hmpc_create(ctypes.byref(h), 3, 7, 0.02, 7.5, 9.807, 1.0, J, r, 0, 0) == -2
+    # horizons without a dedicated kernel run on the generic one up to N = 128
+    assert lib.hmpc_create(ctypes.byref(h), 3, 129, 0.02, 7.5, 9.807, 1.0, J, r, 0, 0) == -2
     assert lib.hmpc_destroy(None) == -1
+    assert lib.hmpc_set_precision(None, 1) == -1
 
 
 def test_missing_library_fails_loudly(tmp_path):
