@@ -295,10 +295,13 @@ __device__ __forceinline__ double tri_fwd(double acc, const double (&Mr)[6 * N],
 }
 // The same sweep from the LDS copy (the active-set phase, where the
 // registers hold the Gram-Schmidt basis instead): loads of step s+4 are
-// issued at step s (a 4-deep ring of hand-counted loads).
+// issued at step s (a 4-deep ring of hand-counted loads).  s0 (uniform, a
+// multiple of 4): b is zero above row s0, so are the first s0 entries of y
+// and the sweep starts there (constraint normals are sparse: a box or
+// friction row of stage j starts at 6j).
 template <int N>
 __device__ __forceinline__ double tri_fwd_lds(double acc, const double* Mc, const double* zero,
-                                              double dinv, double* red) {
+                                              double dinv, double* red, int s0 = 0) {
   using L = Lay<N>;
   constexpr int NV = L::NV;
   constexpr int SEND = (NV + 3) & ~3;   // padded (steps >= NV are no-ops)
@@ -311,10 +314,10 @@ __device__ __forceinline__ double tri_fwd_lds(double acc, const double* Mc, cons
     };
     double ring[4];
     sfor<0, 4>([&](auto jc) __attribute__((always_inline)) {
-      lds_ld64(ring[decltype(jc)::value], addr(decltype(jc)::value));
+      lds_ld64(ring[decltype(jc)::value], addr(s0 + decltype(jc)::value));
     });
 #pragma unroll 1
-    for (int s = 0; s < SEND; s += 4) {
+    for (int s = s0; s < SEND; s += 4) {
       sfor<0, 4>([&](auto jc) __attribute__((always_inline)) {
         constexpr int j = decltype(jc)::value;
         const int sj = s + j;
@@ -343,8 +346,8 @@ __device__ __forceinline__ double tri_fwd_lds(double acc, const double* Mc, cons
     double r0[4], r1[4];
     sfor<0, 4>([&](auto jc) __attribute__((always_inline)) {
       constexpr int j = decltype(jc)::value;
-      lds_ld64(r0[j], ad0(j));
-      lds_ld64(r1[j], ad1(j));
+      lds_ld64(r0[j], ad0(s0 + j));
+      lds_ld64(r1[j], ad1(s0 + j));
     });
     auto steps = [&](int s, const double& src, int off) __attribute__((always_inline)) {
       sfor<0, 4>([&](auto jc) __attribute__((always_inline)) {
@@ -359,9 +362,9 @@ __device__ __forceinline__ double tri_fwd_lds(double acc, const double* Mc, cons
       });
     };
 #pragma unroll 1
-    for (int s = 0; s < 64; s += 4) steps(s, a0, 0);
+    for (int s = s0; s < 64; s += 4) steps(s, a0, 0);
 #pragma unroll 1
-    for (int s = 64; s < SEND; s += 4) steps(s, a1, 64);
+    for (int s = (s0 > 64 ? s0 : 64); s < SEND; s += 4) steps(s, a1, 64);
     lds_wait<0>(r0[0], r1[0]);   // drain the ring (its last loads are dummies)
     acc = tid < 64 ? a0 : a1;
   }
@@ -450,10 +453,17 @@ __device__ __forceinline__ double tri_bwd(double acc, const double* Mc, const do
 // product build compiles these to nothing.
 #ifdef HMPC_STAMPS
 #define HMPC_STAMP(i) (stamp_[i] = __builtin_amdgcn_s_memtime())
+// accumulated sub-phase timers of the active set (slots 9..14)
+#define HMPC_TIC(v) const long long v = __builtin_amdgcn_s_memtime()
+#define HMPC_TOC(slot, v) (stamp_[slot] += __builtin_amdgcn_s_memtime() - (v))
 #elif defined(HMPC_MARKS)   // phase markers in the .s (register-pressure work)
 #define HMPC_STAMP(i) asm volatile(";@@PHASE " #i)
 #else
 #define HMPC_STAMP(i) ((void)0)
+#endif
+#ifndef HMPC_STAMPS
+#define HMPC_TIC(v) ((void)0)
+#define HMPC_TOC(slot, v) ((void)0)
 #endif
 
 #ifndef HMPC_WAVES_PER_EU
@@ -1055,6 +1065,7 @@ solve_kernel(SolveArgs a) {
   bool done = status != ST_SOLVED;
   while (!done) {
     // ---- slacks of my constraints; pick the most violated ----
+    HMPC_TIC(t_scan);
     xs[tid] = v;
     B::sync();
     // branch-free: slots 0/1 are +-a0 v + muf fz_stage + k0/k1; slot 2 the
@@ -1079,14 +1090,18 @@ solve_kernel(SolveArgs a) {
     if (nslots > 1 && !(actmask & 2)) argmin_combine(best, bid, sc1, 4 * tid + 1);
     if (nslots > 2 && !(actmask & 4)) argmin_combine(best, bid, sc2, 4 * tid + 2);
     B::argmin(best, bid, red);
+    HMPC_TOC(9, t_scan);
     if (!(best < -kTol)) break;   // primal feasible: optimal
     const int p = uni(bid);
     const double bp = rhs_of(p);
     const double np_me = coef_of(p, tid);
     double u_plus = 0.0;
     // w = L^-1 n_p
-    const double wfull = tri_fwd_lds<N>(np_me, Lc, zero, dinv, xs);
+    HMPC_TIC(t_fwd);
+    const int s0 = B::first(np_me != 0.0, red);   // first nonzero of n_p (-1: none)
+    const double wfull = tri_fwd_lds<N>(np_me, Lc, zero, dinv, xs, s0 > 0 ? (s0 & ~3) : 0);
     const double wnorm2 = B::sum(wfull * wfull, red);
+    HMPC_TOC(10, t_fwd);
 
     // ---- inner loop: step towards satisfying constraint p ----
     while (true) {
@@ -1094,6 +1109,7 @@ solve_kernel(SolveArgs a) {
       const int qu = uni(q);
       // w_perp = (I - Qw Qw') w and c = Qw' w by modified Gram-Schmidt; a
       // second pass when the first one cancels more than half the norm
+      HMPC_TIC(t_gs);
       double wp = wfull, zn = wnorm2;
 #pragma unroll 1
       for (int pass = 0; pass < 2 && qu > 0; ++pass) {
@@ -1125,8 +1141,12 @@ solve_kernel(SolveArgs a) {
         if (enough) break;
       }
       B::sync();
+      HMPC_TOC(11, t_gs);
       // primal direction z = L^-T w_perp (lane v gets z_v)
+      HMPC_TIC(t_bwd);
       const double zi = tri_bwd<N>(wp, Lc, zero, dinv, xs);
+      HMPC_TOC(12, t_bwd);
+      HMPC_TIC(t_dual);
       // dual direction r = R^-1 c (lanes l < q), back substitution
       double rcur = tid < qu ? cbv[tid] : 0.0, rmine = 0.0;
       for (int l = qu - 1; l >= 0; --l) {
@@ -1149,6 +1169,8 @@ solve_kernel(SolveArgs a) {
       if (tid < qu) ua[tid] -= t * rmine;
       u_plus += t;
       B::sync();
+      HMPC_TOC(13, t_dual);
+      HMPC_TIC(t_upd);
       if (has_z && t == t2) {
         // ---- add p: new basis column w_perp / |w_perp|, R column [c; rho] ----
         if (qu >= QMAX) { status = ST_NUMERICAL; done = true; break; }
@@ -1165,6 +1187,7 @@ solve_kernel(SolveArgs a) {
         if (tid == (p >> 2)) actmask |= 1 << (p & 3);
         q = qu + 1;
         B::sync();
+        HMPC_TOC(14, t_upd);
         break;
       }
       // ---- drop active constraint kdrop ----
@@ -1219,6 +1242,7 @@ solve_kernel(SolveArgs a) {
         for (int l = 0; l < QMAX; ++l) Qw[l] = (l == qu - 1) ? 0.0 : Qw[l];
         q = qu - 1;
         B::sync();
+        HMPC_TOC(14, t_upd);
       }
     }
   }
@@ -1278,7 +1302,7 @@ solve_kernel(SolveArgs a) {
 #else
     HMPC_STAMP(8);
     if (a.x && tid == 0)
-      for (int i = 0; i < 12; ++i)
+      for (int i = 0; i < 16; ++i)
         reinterpret_cast<long long*>(a.x)[b * 12 * (N + 1) + i] = stamp_[i];
 #endif
     if (tid == 0) {

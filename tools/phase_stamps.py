@@ -43,6 +43,11 @@ def main():
     res['total_p50'] = float(np.median(tot))
     res['total_max'] = float(tot.max())
     res['iters_mean'] = float(out['iters'].float().mean())
+    # accumulated active-set sub-phases (slots 9..14 of the stamped build)
+    acc = out['x'].view(torch.int64).reshape(B, -1)[:, 9:15].cpu().numpy()
+    for i, n in enumerate(['gi_scan', 'gi_fwd_sweep', 'gi_gram_schmidt', 'gi_bwd_sweep',
+                           'gi_dual_step', 'gi_add_drop']):
+        res[n] = float(acc[:, i].mean())
     print(json.dumps(res, indent=1))
 
 
