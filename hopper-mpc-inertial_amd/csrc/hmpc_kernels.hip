@@ -499,27 +499,61 @@ solve_kernel(SolveArgs a) {
     reinterpret_cast<const double**>(sm + L::XRV)[0] = xrf;
     reinterpret_cast<int*>(sm + L::XRV + 1)[0] = a.xref_rs;
   }
-  for (int i = tid; i < 12; i += NT) sm[L::XIN + i] = a.x_in[b * 12 + i];
-  for (int i = tid; i < 12 * N; i += NT) {
-    const int r = i / 12, c = i - 12 * r;
-    sm[L::XREF + i] = xrf[r * a.xref_rs + c];
-  }
-  for (int i = tid; i < 3 * N; i += NT) {
-    const int r = i / 3, c = i - 3 * r;
-    sm[L::PF + i] = a.pf[b * a.pf_bs + r * a.pf_rs + c];
-  }
-  for (int i = tid; i < N; i += NT) sm[L::CC + i] = a.C[b * a.C_bs + i];
-  if (a.shift_mode == 0) {
-    for (int i = tid; i < 12 * N; i += NT) sm[L::XLIN + i] = a.x_lin[b * 12 * (N + 1) + i];
-  } else if (a.shift_mode == 1) {   // [x_in; x_ref]          (3f :52-53)
-    __syncthreads();
-    for (int i = tid; i < 12 * N; i += NT)
-      sm[L::XLIN + i] = i < 12 ? sm[L::XIN + i] : sm[L::XREF + i - 12];
-  } else {                          // [x_in; x_prev[2:]; x_prev[N]]  (3f :59-62)
+  // Every global load is issued before the first LDS store (one memory
+  // round trip instead of one per array); out-of-range lanes load element 0
+  // of their array and discard it.
+  {
+    constexpr int NR = (12 * N + NT - 1) / NT, NP = (3 * N + NT - 1) / NT, NCC = (N + NT - 1) / NT;
     const double* xp = a.x_lin + b * 12 * (N + 1);
-    for (int i = tid; i < 12 * N; i += NT) {
-      const int r = i / 12, c = i - 12 * r;
-      sm[L::XLIN + i] = (r == 0) ? a.x_in[b * 12 + c] : xp[(r + 1) * 12 + c];   // r+1 <= N
+    const int mode = a.shift_mode;
+    double vi, vr[NR], vp[NP], vc[NCC], vl[NR];
+    vi = a.x_in[b * 12 + (tid < 12 ? tid : 0)];
+    sfor<0, NR>([&](auto itc) __attribute__((always_inline)) {
+      constexpr int it = decltype(itc)::value;
+      const int i = tid + it * NT, ic = i < 12 * N ? i : 0;
+      const int r = ic / 12, c = ic - 12 * r;
+      vr[it] = xrf[r * a.xref_rs + c];
+      // x_lin rows 0..N-1: given (mode 0) or the time shift of x_prev
+      // (mode 2: [x_in; x_prev[2:]; x_prev[N]], 3f :59-62; row 0 is x_in,
+      // which lane i < 12 already holds in vi)
+      vl[it] = xp[mode == 0 ? ic : ((r + 1 <= N ? r + 1 : N) * 12 + c)];
+    });
+    sfor<0, NP>([&](auto itc) __attribute__((always_inline)) {
+      constexpr int it = decltype(itc)::value;
+      const int i = tid + it * NT, ic = i < 3 * N ? i : 0;
+      const int r = ic / 3, c = ic - 3 * r;
+      vp[it] = a.pf[b * a.pf_bs + r * a.pf_rs + c];
+    });
+    sfor<0, NCC>([&](auto itc) __attribute__((always_inline)) {
+      constexpr int it = decltype(itc)::value;
+      const int i = tid + it * NT;
+      vc[it] = a.C[b * a.C_bs + (i < N ? i : 0)];
+    });
+    const double mu_b = a.mu ? a.mu[b] : a.mu_default;
+    if (tid < 12) sm[L::XIN + tid] = vi;
+    if (tid == 0) sm[L::ZR + 1] = mu_b;   // read again in phase 6
+    sfor<0, NR>([&](auto itc) __attribute__((always_inline)) {
+      constexpr int it = decltype(itc)::value;
+      const int i = tid + it * NT;
+      if (i < 12 * N) {
+        sm[L::XREF + i] = vr[it];
+        if (mode != 1) sm[L::XLIN + i] = (mode == 2 && i < 12) ? vi : vl[it];
+      }
+    });
+    sfor<0, NP>([&](auto itc) __attribute__((always_inline)) {
+      constexpr int it = decltype(itc)::value;
+      const int i = tid + it * NT;
+      if (i < 3 * N) sm[L::PF + i] = vp[it];
+    });
+    sfor<0, NCC>([&](auto itc) __attribute__((always_inline)) {
+      constexpr int it = decltype(itc)::value;
+      const int i = tid + it * NT;
+      if (i < N) sm[L::CC + i] = vc[it];
+    });
+    if (mode == 1) {   // [x_in; x_ref]   (3f :52-53)
+      __syncthreads();
+      for (int i = tid; i < 12 * N; i += NT)
+        sm[L::XLIN + i] = i < 12 ? sm[L::XIN + i] : sm[L::XREF + i - 12];
     }
   }
   __syncthreads();
@@ -970,7 +1004,7 @@ solve_kernel(SolveArgs a) {
 
   // per-instance scalars needed after the factorisation are re-derived here
   // rather than kept live across it (they were spilled there)
-  const double mu = a.mu ? a.mu[b] : a.mu_default;
+  const double mu = sm[L::ZR + 1];   // staged in phase 0
   const double dtm2 = dt / a.m + 0.0 * (double)opaque_zero();
   // stage / component of my variable, recomputed from an opaque thread id:
   // phase 3's copies would stay alive (spilled) across the factorisation
