@@ -879,15 +879,22 @@ solve_kernel(SolveArgs a) {
         }
         Rg[k] = below ? tk : 0.0;
         const unsigned cbase = lds_addr(sm + L::COLB + (k & 1) * (NT + 8) + JA);
-        dbl2 buf[2][CW / 2];
+        // chunks >= 1 go through a 3-deep ring: chunk ch+2 is issued while
+        // chunk ch is consumed (one chunk ahead left the LDS latency exposed)
+        dbl2 buf[3][CW / 2];
         auto load = [&](auto chc) __attribute__((always_inline)) {
           constexpr int ch = decltype(chc)::value;
           if constexpr (ch >= 1 && ch < NCH) {
             sfor<0, nldc(JA, ch)>([&](auto ic) __attribute__((always_inline)) {
               constexpr int i = decltype(ic)::value;
-              lds_ld128<8 * CW * ch + 16 * i>(buf[ch % 2][i], cbase);
+              lds_ld128<8 * CW * ch + 16 * i>(buf[ch % 3][i], cbase);
             });
           }
+        };
+        auto nl = [](int ja, int ch) constexpr {   // loads of chunk ch (0 beyond the row)
+          return (ch >= 1 && ch < (NV - ja + CW - 1) / CW) ? ((NV - ja - CW * ch) >= CW ? CW / 2
+                                                                 : (NV - ja - CW * ch + 1) / 2)
+                                                           : 0;
         };
         auto update = [&](auto chc, const dbl2 (&bf)[CW / 2]) __attribute__((always_inline)) {
           constexpr int ch = decltype(chc)::value;
@@ -905,18 +912,21 @@ solve_kernel(SolveArgs a) {
           const bool run = !kforce || !((fixmask >> k) & 1);   // uniform
           if (run) {
             load(std::integral_constant<int, 1>{});
+            load(std::integral_constant<int, 2>{});
             if constexpr (NCH > 0) update(std::integral_constant<int, 0>{}, nb);
           }
           if constexpr (k + 1 < NV) ahead(std::integral_constant<int, k + 1>{});
           if (run) {
             sfor<1, NCH>([&](auto chc) __attribute__((always_inline)) {
               constexpr int ch = decltype(chc)::value;
-              load(std::integral_constant<int, ch + 1>{});
-              // LDS ops issued after chunk ch's loads: chunk ch+1, and for
-              // ch == 1 also ahead()'s column store and loads
-              constexpr int younger = (ch + 1 < NCH ? nldc(JA, ch + 1) : 0) + (ch == 1 ? NAHEAD : 0);
-              lds_wait<younger>(buf[ch % 2][0], buf[ch % 2][1]);
-              update(chc, buf[ch % 2]);
+              load(std::integral_constant<int, ch + 2>{});
+              // LDS ops issued after chunk ch's loads (issue order: chunks 1,
+              // 2, ahead(), then chunk c+2 at iteration c)
+              constexpr int younger = ch == 1 ? nl(JA, 2) + NAHEAD + nl(JA, 3)
+                                    : ch == 2 ? NAHEAD + nl(JA, 3) + nl(JA, 4)
+                                              : nl(JA, ch + 1) + nl(JA, ch + 2);
+              lds_wait<younger>(buf[ch % 3][0], buf[ch % 3][1]);
+              update(chc, buf[ch % 3]);
             });
           }
         } else {
