@@ -26,7 +26,7 @@ $HIPCC $FLAGS -c csrc/hmpc_capi.cpp -o $BDIR/hmpc_capi.o &
 pids+=($!)
 $HIPCC $FLAGS -c csrc/hmpc_plant.hip -o $BDIR/hmpc_plant.o &
 pids+=($!)
-$HIPCC $FLAGS -c csrc/hmpc_wide.hip -o $BDIR/hmpc_wide.o &
+$HIPCC $FLAGS -c csrc/hmpc_wide.hip -o $BDIR/hmpc_wide.o "$@" &
 pids+=($!)
 for p in "${pids[@]}"; do wait "$p"; done
 objs=""

@@ -41,6 +41,7 @@ namespace {
 constexpr int WT = 256;               // threads per workgroup
 constexpr int WW = WT / 64;           // waves
 constexpr int NVMAX = 6 * kWideNmax;  // LDS vectors
+constexpr int kPanelElems = 6144;     // NV x PB: PB = 16 up to NV = 384, else 8
 
 template <typename T>
 struct Shared {
@@ -48,6 +49,7 @@ struct Shared {
   int ired[WW];
   T vec[NVMAX];   // a broadcast vector (Cholesky column, d, Householder v)
   T vec2[NVMAX];
+  T pan[kPanelElems];   // Cholesky panel (rows k0.., PB columns)
   T npv[kWideNmax + 2];   // n_p: <= N nonzeros (z rows), else <= 2
   int npi[kWideNmax + 2];
   int npn;
@@ -101,8 +103,18 @@ __device__ void rows_dot(const T* M, int ld, int n, int k0, const T* vec, T* out
 
 __device__ __forceinline__ void gfence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup"); }
 
+#ifdef HMPC_STAMPS
+#define WSTAMP(i) (wst[i] = __builtin_amdgcn_s_memtime())
+#else
+#define WSTAMP(i) ((void)0)
+#endif
+
 template <int VAR, typename T>
 __device__ void wide_solve(const SolveArgs& a, const int N, const int64_t b, T* ws, Shared<T>& sh) {
+#ifdef HMPC_STAMPS
+  long long wst[10] = {0};
+#endif
+  WSTAMP(0);
   const WideLayout Lw(N);
   const int tid = threadIdx.x;
   const int NV = 6 * N;
@@ -159,10 +171,12 @@ __device__ void wide_solve(const SolveArgs& a, const int N, const int64_t b, T* 
     gfence();
     __syncthreads();
   }
+  WSTAMP(1);
   // ---------------- 1: gen_dt_dynamics --------------------------------------
   for (int k = tid; k < N; k += WT) stage_dynamics<VAR>(k, xl, pf, a.Jinv, a.rh, dt, cs, bw);
   gfence();
   __syncthreads();
+  WSTAMP(2);
   // ---------------- 2: free response, S_t, adjoint (wave 0) -----------------
   if (tid < 64) {
     T xrr = tid < 12 ? xin[tid] : T(0.0);
@@ -230,6 +244,7 @@ __device__ void wide_solve(const SolveArgs& a, const int N, const int64_t b, T* 
       if (tid >= 6 && tid < 12) aj[6 * (t - 1) + tid - 6] = ar;
     }
   }
+  WSTAMP(3);
   // ---------------- 3: free variables, Hessian rows, gradient ----------------
   if (tid == 0) {
     int nf = 0;
@@ -283,42 +298,173 @@ __device__ void wide_solve(const SolveArgs& a, const int N, const int64_t b, T* 
   __syncthreads();
 
   int status = ST_SOLVED;
+  WSTAMP(4);
   // ---------------- 4: Cholesky --------------------------------------------
-  for (int k = 0; k < NF; ++k) {
-    const T piv = H[(int64_t)k * ld + k];
-    if (!(piv > T(0.0))) { status = ST_NUMERICAL; break; }
-    const T lkk = sqrt(piv), rl = T(1.0) / lkk;
-    for (int i = k + 1 + tid; i < NF; i += WT) {
-      const T l = H[(int64_t)i * ld + k] * rl;
-      H[(int64_t)i * ld + k] = l;
-      sh.vec[i] = l;
-    }
-    gfence();
-    __syncthreads();   // every thread has read the pivot; column k published
-    if (tid == 0) H[(int64_t)k * ld + k] = lkk;
-    for (int i = k + 1; i < NF; ++i) {
-      const T li = sh.vec[i];
-      T* Hi = H + (int64_t)i * ld;
-      for (int j = k + 1 + tid; j <= i; j += WT) Hi[j] = fma(-li, sh.vec[j], Hi[j]);
-    }
-    gfence();
-    __syncthreads();
-  }
-  // ---------------- 5: J = L^-T (row c of J = column c of L^-1) -------------
-  if (status == ST_SOLVED) {
-    for (int c = tid; c < NF; c += WT) {
-      T* Jc = J + (int64_t)c * ld;
-      for (int i = 0; i < c; ++i) Jc[i] = T(0.0);
-      for (int i = c; i < NF; ++i) {
-        const T* Li = H + (int64_t)i * ld;
-        T acc = (i == c) ? T(1.0) : T(0.0);
-        for (int k = c; k < i; ++k) acc = fma(-Li[k], Jc[k], acc);
-        Jc[i] = acc / Li[i];
+  // Blocked right-looking: a panel of PB columns is factored in LDS, written
+  // back, and the trailing lower triangle gets one rank-PB update by 4 x 4
+  // register tiles -- one pass over the trailing matrix per panel instead
+  // of one per column.
+  {
+    const int PB = NV <= 384 ? 16 : 8;
+    T* P = sh.pan;
+    for (int k0 = 0; k0 < NF && status == ST_SOLVED; k0 += PB) {
+      const int pw = NF - k0 < PB ? NF - k0 : PB;
+      const int m = NF - k0;
+      for (int e = tid; e < m * PB; e += WT) {
+        const int r = e / PB, c = e - PB * r;
+        P[e] = (c < pw && c <= r) ? H[(int64_t)(k0 + r) * ld + k0 + c] : T(0);
       }
+      __syncthreads();
+      for (int c = 0; c < pw; ++c) {
+        const T piv = P[c * PB + c];
+        if (!(piv > T(0))) { status = ST_NUMERICAL; break; }   // uniform
+        const T lkk = sqrt(piv), rl = T(1) / lkk;
+        __syncthreads();   // every thread has read the pivot
+        for (int r = c + 1 + tid; r < m; r += WT) P[r * PB + c] *= rl;
+        if (tid == 0) P[c * PB + c] = lkk;
+        __syncthreads();
+        const int nc = pw - c - 1;
+        if (nc > 0) {
+          for (int e = tid; e < (m - c - 1) * nc; e += WT) {
+            const int rr = c + 1 + e / nc, cc = c + 1 + e % nc;
+            if (rr >= cc) P[rr * PB + cc] = fma(-P[rr * PB + c], P[cc * PB + c], P[rr * PB + cc]);
+          }
+          __syncthreads();
+        }
+      }
+      if (status != ST_SOLVED) break;
+      for (int e = tid; e < m * PB; e += WT) {
+        const int r = e / PB, c = e - PB * r;
+        if (c < pw && c <= r) H[(int64_t)(k0 + r) * ld + k0 + c] = P[e];
+      }
+      // trailing rank-pw update of rows/cols >= k0 + pw, 4 x 4 tiles
+      const int t0 = k0 + pw, mt = NF - t0;
+      const int T4 = (mt + 3) / 4;
+      const int ntile = T4 * (T4 + 1) / 2;
+      for (int tp = tid; tp < ntile; tp += WT) {
+        int ti = (int)((sqrtf(8.0f * (float)tp + 1.0f) - 1.0f) * 0.5f);
+        while (ti * (ti + 1) / 2 > tp) --ti;
+        while ((ti + 1) * (ti + 2) / 2 <= tp) ++ti;
+        const int tj = tp - ti * (ti + 1) / 2;
+        const int i0 = t0 + 4 * ti, j0 = t0 + 4 * tj;
+        T acc[4][4];
+#pragma unroll
+        for (int a2 = 0; a2 < 4; ++a2)
+#pragma unroll
+          for (int b2 = 0; b2 < 4; ++b2) acc[a2][b2] = T(0);
+        for (int c = 0; c < pw; ++c) {
+          T av[4], bvv[4];
+#pragma unroll
+          for (int a2 = 0; a2 < 4; ++a2) {
+            const int ri = i0 + a2 - k0, rj = j0 + a2 - k0;
+            av[a2] = ri < m ? P[ri * PB + c] : T(0);
+            bvv[a2] = rj < m ? P[rj * PB + c] : T(0);
+          }
+#pragma unroll
+          for (int a2 = 0; a2 < 4; ++a2)
+#pragma unroll
+            for (int b2 = 0; b2 < 4; ++b2) acc[a2][b2] = fma(av[a2], bvv[b2], acc[a2][b2]);
+        }
+#pragma unroll
+        for (int a2 = 0; a2 < 4; ++a2) {
+          const int ii = i0 + a2;
+          if (ii >= NF) continue;
+          T* Hi = H + (int64_t)ii * ld;
+#pragma unroll
+          for (int b2 = 0; b2 < 4; ++b2) {
+            const int jj = j0 + b2;
+            if (jj <= ii) Hi[jj] -= acc[a2][b2];
+          }
+        }
+      }
+      gfence();
+      __syncthreads();
     }
+  }
+  WSTAMP(5);
+  // ---------------- 5: J = L^-T (row c of J = column c of L^-1) -------------
+  // Y = L^-1 by blocks of rows: a block's rows first take the contribution of
+  // every earlier block (4 x 4 register tiles over rows of L staged in LDS and
+  // rows of J = Y'), then a short forward substitution inside the block, one
+  // thread per column (no barrier: a column's entries are that thread's).
+  if (status == ST_SOLVED) {
+    for (int64_t e = tid; e < (int64_t)NF * ld; e += WT) J[e] = T(0);
     gfence();
     __syncthreads();
+    const int RB = NV <= 384 ? 16 : 8;
+    T* Lb = sh.pan;   // rows rb..re-1 of L, columns 0..re-1 (stride re)
+    for (int rb = 0; rb < NF; rb += RB) {
+      const int re = NF - rb < RB ? NF : rb + RB;
+      const int h = re - rb;
+      for (int e = tid; e < h * re; e += WT) {
+        const int r = e / re, k = e - re * r;
+        Lb[e] = (k <= rb + r) ? H[(int64_t)(rb + r) * ld + k] : T(0);
+      }
+      __syncthreads();
+      // A: J[c][rb + r] = delta(rb + r, c) - sum_{k < rb} L[rb + r][k] Y[k][c]
+      const int TC = (re + 3) / 4, TR = (h + 3) / 4;
+      for (int tp = tid; tp < TR * TC; tp += WT) {
+        const int tr = tp / TC, tc = tp - TC * tr;
+        const int r0 = 4 * tr, c0 = 4 * tc;
+        T acc[4][4];
+#pragma unroll
+        for (int a2 = 0; a2 < 4; ++a2)
+#pragma unroll
+          for (int b2 = 0; b2 < 4; ++b2) acc[a2][b2] = T(0);
+        const T* Jc[4];
+#pragma unroll
+        for (int b2 = 0; b2 < 4; ++b2) Jc[b2] = J + (int64_t)(c0 + b2 < re ? c0 + b2 : c0) * ld;
+        for (int k = c0; k < rb; ++k) {   // Y[k][c] = 0 for k < c
+          T av[4], bvv[4];
+#pragma unroll
+          for (int a2 = 0; a2 < 4; ++a2) av[a2] = r0 + a2 < h ? Lb[(r0 + a2) * re + k] : T(0);
+#pragma unroll
+          for (int b2 = 0; b2 < 4; ++b2) bvv[b2] = Jc[b2][k];
+#pragma unroll
+          for (int a2 = 0; a2 < 4; ++a2)
+#pragma unroll
+            for (int b2 = 0; b2 < 4; ++b2) acc[a2][b2] = fma(av[a2], bvv[b2], acc[a2][b2]);
+        }
+#pragma unroll
+        for (int a2 = 0; a2 < 4; ++a2) {
+          const int r = rb + r0 + a2;
+          if (r0 + a2 >= h) continue;
+#pragma unroll
+          for (int b2 = 0; b2 < 4; ++b2) {
+            const int c = c0 + b2;
+            if (c < re) J[(int64_t)c * ld + r] = ((r == c) ? T(1) : T(0)) - acc[a2][b2];
+          }
+        }
+      }
+      gfence();
+      __syncthreads();
+      // B: forward substitution inside the block, column c per thread, the
+      // block's entries of the column in registers (rows above c are 0 and
+      // stay 0, so every column runs the same unrolled triangle)
+      for (int c = tid; c < re; c += WT) {
+        T* Jcol = J + (int64_t)c * ld + rb;
+        T y[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) y[r] = r < h ? Jcol[r] : T(0);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          if (r < h) {
+            const T* Lr = Lb + r * re + rb;
+            T acc = y[r];
+#pragma unroll
+            for (int k = 0; k < r; ++k) acc = fma(-Lr[k], y[k], acc);
+            y[r] = acc / Lr[r];
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (r < h) Jcol[r] = y[r];
+      }
+      gfence();
+      __syncthreads();
+    }
   }
+  WSTAMP(6);
   // ---------------- 6: Goldfarb-Idnani -------------------------------------
   int iters = 0;
   const T mu = T(a.mu ? a.mu[b] : a.mu_default);
@@ -545,6 +691,7 @@ __device__ void wide_solve(const SolveArgs& a, const int N, const int64_t b, T* 
       __syncthreads();
     }
   }
+  WSTAMP(7);
   // ---------------- 7: outputs ---------------------------------------------
   for (int v = tid; v < NV; v += WT) {
     const T u = (status == ST_SOLVED && pos[v] >= 0) ? xv[pos[v]] : T(0.0);
@@ -588,6 +735,11 @@ __device__ void wide_solve(const SolveArgs& a, const int N, const int64_t b, T* 
       if (xo && tid < 12) xo[12 * (k + 1) + tid] = xrr;
     }
     const T objv = wave_sum(objl);
+#ifdef HMPC_STAMPS
+    WSTAMP(8);
+    if (xo && tid == 0)
+      for (int i = 0; i < 9; ++i) reinterpret_cast<long long*>(xo)[i] = wst[i];
+#endif
     if (tid == 0) {
       if (a.obj) a.obj[b] = objv;
       a.status[b] = status;
