@@ -47,8 +47,9 @@ struct SolveArgs {
 // Horizons without a dedicated kernel run on the generic kernel up to this N.
 constexpr int kWideNmax = 128;
 
-// Per-instance workspace of the generic-horizon kernel, in doubles.  The
-// three NV x NV blocks (H -> L, J = L^-T Q, R) dominate: 3 MB at N = 60.
+// Per-instance workspace of the generic-horizon kernel, in elements of its
+// arithmetic type.  The two NV x NV blocks (H -> L, J = L^-T Q) dominate:
+// 2.1 MB at N = 60 in fp64.
 struct WideLayout {
   int64_t XIN, CC, CS, BW, ZB, XL, XR, PF, SS, DG, AJ;         // per stage
   int64_t HV, XV, DV, ZV, WV, UO, RV, UA, FR, POS, ACT, ISA;   // per variable
@@ -80,7 +81,7 @@ struct WideLayout {
     POS = o; o = up(o + NV);
     ACT = o; o = up(o + NV + 1);
     ISA = o; o = up(o + 4 * NV);
-    RM = o; o = up(o + NV * NV);
+    RM = o;   // (R lives in LDS; kept for layout compatibility, no space)
     H = o; o = up(o + NV * NV);
     J = o; o = up(o + NV * NV);
     total = o;

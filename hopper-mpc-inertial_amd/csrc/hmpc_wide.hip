@@ -42,6 +42,7 @@ constexpr int WT = 256;               // threads per workgroup
 constexpr int WW = WT / 64;           // waves
 constexpr int NVMAX = 6 * kWideNmax;  // LDS vectors
 constexpr int kPanelElems = 6144;     // NV x PB: PB = 16 up to NV = 384, else 8
+constexpr int QL = 78;                // active-set capacity: R (QL x QL) lives in the panel buffer
 
 template <typename T>
 struct Shared {
@@ -142,7 +143,6 @@ __device__ void wide_solve(const SolveArgs& a, const int N, const int64_t b, T* 
   int* pos = reinterpret_cast<int*>(ws + Lw.POS);
   int* act = reinterpret_cast<int*>(ws + Lw.ACT);
   int* isa = reinterpret_cast<int*>(ws + Lw.ISA);
-  T* Rm = ws + Lw.RM;
   T* H = ws + Lw.H;
   T* J = ws + Lw.J;
   const int ld = NV;   // row stride of H, J, R
@@ -467,6 +467,7 @@ __device__ void wide_solve(const SolveArgs& a, const int N, const int64_t b, T* 
   WSTAMP(6);
   // ---------------- 6: Goldfarb-Idnani -------------------------------------
   int iters = 0;
+  T* Rl = sh.pan;   // R, q x q upper, stride QL (the Cholesky panel buffer is free now)
   const T mu = T(a.mu ? a.mu[b] : a.mu_default);
   const T zc = dt * dtm;   // coefficient scale of fz_j in z_k (Bd[8][2] = dt/m)
   if (xin[2] - T(kZmin) < -tol || zb[1] - T(kZmin) < -tol) status = ST_INFEAS;   // constant rows z_0, z_1
@@ -585,8 +586,8 @@ __device__ void wide_solve(const SolveArgs& a, const int N, const int64_t b, T* 
       if (tid == 0) {
         for (int i = q - 1; i >= 0; --i) {
           T t = sh.vec[i];
-          for (int k = i + 1; k < q; ++k) t = fma(-Rm[(int64_t)i * ld + k], rv[k], t);
-          rv[i] = t / Rm[(int64_t)i * ld + i];
+          for (int k = i + 1; k < q; ++k) t = fma(-Rl[i * QL + k], rv[k], t);
+          rv[i] = t / Rl[i * QL + i];
         }
         T t1 = INFINITY;
         int kd = -1;
@@ -615,6 +616,7 @@ __device__ void wide_solve(const SolveArgs& a, const int N, const int64_t b, T* 
       __syncthreads();
       if (has_z && t == t2) {
         // ---- add p: one Householder reflection maps d2 onto alpha e_q ----
+        if (q >= QL) { status = ST_NUMERICAL; done = true; break; }   // uniform
         const T dq = sh.vec[q];
         const T alpha = sqrt(zz);
         const T sg = dq >= T(0.0) ? T(1.0) : -T(1.0);
@@ -626,18 +628,21 @@ __device__ void wide_solve(const SolveArgs& a, const int N, const int64_t b, T* 
         __syncthreads();
         // J2 <- J2 (I - beta v v'); column q flips sign when sg > 0 so that
         // the new R diagonal is +alpha
-        for (int i = 0; i < NF; ++i) {
-          T* Ji = J + (int64_t)i * ld;
-          const T bwi = beta * wv[i];
-          for (int k = q + tid; k < NF; k += WT) {
-            T x = fma(-bwi, sh.vec2[k], Ji[k]);
-            if (k == q && sg > T(0.0)) x = -x;
-            Ji[k] = x;
+        // (a thread per column k, rows streamed: coalesced over k, independent
+        // rows in flight)
+        for (int k = q + tid; k < NF; k += WT) {
+          const T vk = beta * sh.vec2[k];
+          const bool flip = (k == q && sg > T(0));
+          T* Jk = J + k;
+#pragma unroll 4
+          for (int i = 0; i < NF; ++i) {
+            const T x = fma(-wv[i], vk, Jk[(int64_t)i * ld]);
+            Jk[(int64_t)i * ld] = flip ? -x : x;
           }
         }
-        for (int i = tid; i < q; i += WT) Rm[(int64_t)i * ld + q] = sh.vec[i];
+        for (int i = tid; i < q; i += WT) Rl[i * QL + q] = sh.vec[i];
         if (tid == 0) {
-          Rm[(int64_t)q * ld + q] = alpha;
+          Rl[q * QL + q] = alpha;
           act[q] = p;
           ua[q] = uplus;
           isa[p] = 1;
@@ -653,21 +658,21 @@ __device__ void wide_solve(const SolveArgs& a, const int N, const int64_t b, T* 
         for (int j = kd; j < q - 1; ++j) {
           act[j] = act[j + 1];
           ua[j] = ua[j + 1];
-          for (int i = 0; i <= j + 1; ++i) Rm[(int64_t)i * ld + j] = Rm[(int64_t)i * ld + j + 1];
+          for (int i = 0; i <= j + 1; ++i) Rl[i * QL + j] = Rl[i * QL + j + 1];
         }
       }
       gfence();
       __syncthreads();
       for (int j = kd; j < q - 1; ++j) {
         if (tid == 0) {
-          const T aa = Rm[(int64_t)j * ld + j], bb = Rm[(int64_t)(j + 1) * ld + j];
+          const T aa = Rl[j * QL + j], bb = Rl[(j + 1) * QL + j];
           const T hh = sqrt(aa * aa + bb * bb);
           T c = T(1.0), s = T(0.0);
           if (hh != T(0.0)) { c = aa / hh; s = bb / hh; }
           for (int k = j; k < q - 1; ++k) {
-            const T r0 = Rm[(int64_t)j * ld + k], r1 = Rm[(int64_t)(j + 1) * ld + k];
-            Rm[(int64_t)j * ld + k] = c * r0 + s * r1;
-            Rm[(int64_t)(j + 1) * ld + k] = -s * r0 + c * r1;
+            const T r0 = Rl[j * QL + k], r1 = Rl[(j + 1) * QL + k];
+            Rl[j * QL + k] = c * r0 + s * r1;
+            Rl[(j + 1) * QL + k] = -s * r0 + c * r1;
           }
           sh.gc = c;
           sh.gs = s;
@@ -685,7 +690,7 @@ __device__ void wide_solve(const SolveArgs& a, const int N, const int64_t b, T* 
         __syncthreads();
       }
       if (tid == 0)
-        for (int i = 0; i < q; ++i) Rm[(int64_t)i * ld + q - 1] = T(0.0);
+        for (int i = 0; i < q; ++i) Rl[i * QL + q - 1] = T(0.0);
       --q;
       gfence();
       __syncthreads();
