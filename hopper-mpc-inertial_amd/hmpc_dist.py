@@ -33,3 +33,79 @@ def allgather_results(obj: torch.Tensor, status: torch.Tensor, out_obj=None, out
         dist.all_gather(list(out_obj.view(world, n).unbind(0)), obj.contiguous())
         dist.all_gather(list(out_status.view(world, n).unbind(0)), status.contiguous())
     return out_obj, out_status
+
+
+class ResultExchange:
+    """The exchange step of a repeated batched solve, pipelined.
+
+    Each slot is ONE byte buffer per rank, ``[obj (8n B) | status (4n B)]``:
+    the solve writes its objective and status straight into the slot's views
+    (``outputs()``), and ``exchange()`` all-gathers the whole buffer -- one
+    collective per step instead of two.  On CUDA/RCCL the all-gather runs on
+    a side stream after an event of the solve's stream, so step k's exchange
+    overlaps step k+1's solve (which writes the other slot); a slot is
+    reused only after its previous all-gather has completed (event wait on
+    the solve stream).  ``results(slot)`` returns every rank's (obj, status)
+    in rank order.  On gloo (the CPU tests) the exchange is synchronous.
+    """
+
+    def __init__(self, n: int, device, nslots: int = 2):
+        self.n, self.world = n, dist.get_world_size()
+        self.device = torch.device(device)
+        self.cuda = self.device.type == 'cuda'
+        self.nslots = nslots
+        self.send = [torch.empty(12 * n, dtype=torch.uint8, device=self.device)
+                     for _ in range(nslots)]
+        self.recv = [torch.empty(self.world * 12 * n, dtype=torch.uint8, device=self.device)
+                     for _ in range(nslots)]
+        self.stream = torch.cuda.Stream(self.device) if self.cuda else None
+        self.done = [None] * nslots
+        self.k = 0
+
+    def outputs(self):
+        """(obj float64 [n], status int32 [n]) views of the next slot's send
+        buffer; the solve stream first waits for that slot's last exchange."""
+        s = self.k % self.nslots
+        if self.cuda and self.done[s] is not None:
+            torch.cuda.current_stream(self.device).wait_event(self.done[s])
+        buf = self.send[s]
+        return buf[:8 * self.n].view(torch.float64), buf[8 * self.n:].view(torch.int32)
+
+    def exchange(self) -> int:
+        """All-gather the slot the last ``outputs()`` handed out; returns it."""
+        s = self.k % self.nslots
+        self.k += 1
+        if self.cuda:
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(self.stream):
+                self.stream.wait_event(ev)
+                self._gather(s)
+                done = torch.cuda.Event()
+                done.record(self.stream)
+            self.done[s] = done
+        else:
+            self._gather(s)
+        return s
+
+    def _gather(self, s):
+        if dist.get_backend() == 'nccl':
+            dist.all_gather_into_tensor(self.recv[s], self.send[s])
+        else:
+            dist.all_gather(list(self.recv[s].view(self.world, 12 * self.n).unbind(0)),
+                            self.send[s])
+
+    def wait(self):
+        """Make the current stream wait for every outstanding exchange."""
+        if self.cuda:
+            cur = torch.cuda.current_stream(self.device)
+            for d in self.done:
+                if d is not None:
+                    cur.wait_event(d)
+
+    def results(self, slot: int):
+        """(obj [world*n] float64, status [world*n] int32) of a slot, rank order."""
+        r = self.recv[slot].view(self.world, 12 * self.n)
+        obj = r[:, :8 * self.n].contiguous().view(torch.float64).reshape(-1)
+        st = r[:, 8 * self.n:].contiguous().view(torch.int32).reshape(-1)
+        return obj, st

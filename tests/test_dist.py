@@ -43,7 +43,17 @@ def _worker(rank, world, port, q):
     import hmpc_dist
     obj, st = _solve(hmpc_dist.shard_start(rank, PER_RANK), PER_RANK)
     oa, sa = hmpc_dist.allgather_results(torch.from_numpy(obj), torch.from_numpy(st))
-    q.put((rank, oa.numpy().copy(), sa.numpy().copy()))
+    # the bench's pipelined exchange: packed [obj | status] slots, two steps
+    ex = hmpc_dist.ResultExchange(PER_RANK, 'cpu')
+    slots = []
+    for step in range(3):
+        o, s = ex.outputs()
+        o.copy_(torch.from_numpy(obj) * (step + 1))
+        s.copy_(torch.from_numpy(st) + step)
+        slots.append(ex.exchange())
+    ex.wait()
+    po, ps = ex.results(slots[2])   # slot 0 again: step 2 overwrote step 0
+    q.put((rank, oa.numpy().copy(), sa.numpy().copy(), po.numpy().copy() / 3, ps.numpy().copy() - 2))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -63,6 +73,8 @@ def test_sharded_allgather_equals_single_process(world):
         p.join(timeout=60)
         assert p.exitcode == 0
     obj_ref, st_ref = _solve(0, PER_RANK * world)
-    for _, oa, sa in res:
+    for _, oa, sa, po, ps in res:
         assert np.array_equal(oa, obj_ref)
         assert np.array_equal(sa, st_ref)
+        assert np.allclose(po, obj_ref, rtol=1e-15, atol=0)
+        assert np.array_equal(ps, st_ref)
