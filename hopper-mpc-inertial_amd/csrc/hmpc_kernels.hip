@@ -279,16 +279,34 @@ __device__ __forceinline__ void sweep_stage(double b, double& a0, double& a1, do
 }
 // y = L^-1 b (lane v holds b_v), M from registers, fully unrolled.
 // Mr[s] = M[tid][s] below the diagonal and 0 on and above it.
-template <int N>
+// The first NLDS columns come from the LDS copy instead (loaded up front):
+// their registers are then dead from the Cholesky step that finishes them,
+// which keeps the factorisation's live set inside the register file (they
+// were the ones spilled to scratch otherwise).
+template <int N, int NLDS = 0>
 __device__ __forceinline__ double tri_fwd(double acc, const double (&Mr)[6 * N], double dinv,
-                                          double* red) {
+                                          double* red, const double* Mc = nullptr,
+                                          const double* zero = nullptr) {
   using L = Lay<N>;
   constexpr int NV = L::NV;
   const int tid = threadIdx.x;
   (void)tid;
+  double ml[NLDS > 0 ? NLDS : 1];
+  if constexpr (NLDS > 0) {
+    sfor<0, NLDS>([&](auto sc) __attribute__((always_inline)) {
+      constexpr int s = decltype(sc)::value;
+      // M[tid][s] for tid > s sits at Mc[cb(s) + tid - s]; other lanes read a 0
+      lds_ld64(ml[s], lds_addr((tid > s && tid < NV) ? Mc + L::cb(s) + tid - s : zero));
+    });
+  }
   sfor<0, NV>([&](auto sc) __attribute__((always_inline)) {
     constexpr int s = decltype(sc)::value;
-    acc = fma(-Mr[s], Blk<L::W>::bcast(acc, s, red), acc);
+    if constexpr (s < NLDS) {
+      lds_wait<NLDS - 1 - s>(ml[s]);
+      acc = fma(-ml[s], Blk<L::W>::bcast(acc, s, red), acc);
+    } else {
+      acc = fma(-Mr[s], Blk<L::W>::bcast(acc, s, red), acc);
+    }
   });
   // lane v's accumulator is final once step v has read it (M[v][s] = 0, s >= v)
   return acc * dinv;
@@ -466,6 +484,10 @@ __device__ __forceinline__ double tri_bwd(double acc, const double* Mc, const do
 #define HMPC_TOC(slot, v) ((void)0)
 #endif
 
+// columns of the phase-5 forward sweep read from LDS (tri_fwd)
+#ifndef HMPC_FWD_NLDS
+#define HMPC_FWD_NLDS 8
+#endif
 #ifndef HMPC_WAVES_PER_EU
 #define HMPC_WAVES_PER_EU(W) ((W) == 1 ? 2 : 1)
 #endif
@@ -1006,7 +1028,7 @@ solve_kernel(SolveArgs a) {
   double v = 0.0;
   {
     double y;
-    if constexpr (W == 1) y = tri_fwd<N>(-xs[tid], Rg, dinv, red);
+    if constexpr (W == 1) y = tri_fwd<N, HMPC_FWD_NLDS>(-xs[tid], Rg, dinv, red, Lc, zero);
     else y = tri_fwd_lds<N>(-xs[tid], Lc, zero, dinv, xs);   // no per-step exchange
     v = tri_bwd<N>(y, Lc, zero, dinv, xs);
   }
