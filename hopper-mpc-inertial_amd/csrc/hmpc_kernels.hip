@@ -675,16 +675,23 @@ solve_kernel(SolveArgs a) {
 #pragma unroll
       for (int e = 0; e < 22; ++e) sm[L::SS + 22 * (N - 1) + e] = s[e];
     }
+    // stage k's yaw cos/sin from lane k (readlane: no LDS round trip in the
+    // recursions' chains); the reference row is fetched one stage ahead
+    const double cpl = tid < N ? sm[L::CS + 2 * tid] : 0.0;
+    const double spl = tid < N ? sm[L::CS + 2 * tid + 1] : 0.0;
+    double xrn = tid < 12 ? sm[L::XREF + tid] : 0.0;
 #pragma unroll 1
     for (int k = 0; k < N; ++k) {
-      const double cp = sm[L::CS + 2 * k], sp = sm[L::CS + 2 * k + 1];
+      const double cp = rdlane(cpl, k), sp = rdlane(spl, k);
+      const double xrk = xrn;
+      xrn = (tid < 12 && k + 1 < N) ? sm[L::XREF + 12 * (k + 1) + tid] : 0.0;
       xr = ad_lane(xr, dt, cp, sp) + ((tid == 8) ? -a.g * dt : 0.0);
       const double kf = (k == N - 1) ? kTermQ : 1.0;
-      if (tid < 12) sm[L::DG + 12 * k + tid] = kf * qr * (xr - sm[L::XREF + 12 * k + tid]);
+      if (tid < 12) sm[L::DG + 12 * k + tid] = kf * qr * (xr - xrk);
       if (tid == 2) sm[L::ZB + k + 1] = xr;
       const int t = N - 1 - k;
       if (t >= 1) {
-        const double ct = sm[L::CS + 2 * t], st = sm[L::CS + 2 * t + 1];
+        const double ct = rdlane(cpl, t), st = rdlane(spl, t);
         // translational axes and yaw: [[a, b], [b, c]] with p' = p + dt v
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -728,10 +735,12 @@ solve_kernel(SolveArgs a) {
     // (the nonzero rows of Bd).
     double ar = tid < 12 ? sm[L::DG + 12 * (N - 1) + tid] : 0.0;
     if (tid >= 6 && tid < 12) sm[L::AJ + 6 * (N - 1) + tid - 6] = ar;
+    double dgn = (tid < 12 && N >= 2) ? sm[L::DG + 12 * (N - 2) + tid] : 0.0;
 #pragma unroll 1
     for (int t = N - 1; t >= 1; --t) {
-      ar = adt_lane(ar, dt, sm[L::CS + 2 * t], sm[L::CS + 2 * t + 1]) +
-           (tid < 12 ? sm[L::DG + 12 * (t - 1) + tid] : 0.0);
+      const double dgt = dgn;
+      dgn = (tid < 12 && t >= 2) ? sm[L::DG + 12 * (t - 2) + tid] : 0.0;
+      ar = adt_lane(ar, dt, rdlane(cpl, t), rdlane(spl, t)) + dgt;
       if (tid >= 6 && tid < 12) sm[L::AJ + 6 * (t - 1) + tid - 6] = ar;
     }
   }

@@ -34,12 +34,54 @@ __device__ __forceinline__ float rdlane(float x, int l) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), l));
 }
 __device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
+// x of lane (r + D) within r's row of 16 lanes (D < 0: lane r - |D|); a DPP
+// row shift -- a VALU modifier, no LDS round trip like a bpermute.  Lanes
+// whose source falls outside their row read 0.
+template <int D>
+__device__ __forceinline__ int row_shift(int x) {
+  static_assert(D != 0 && D > -16 && D < 16, "row shift");
+  constexpr int ctrl = D > 0 ? 0x100 + D : 0x110 - D;   // row_shl:D / row_shr:-D
+  return __builtin_amdgcn_update_dpp(0, x, ctrl, 0xf, 0xf, true);
+}
+template <int D>
+__device__ __forceinline__ double row_shift(double x) {
+  const long long b = __double_as_longlong(x);
+  const int lo = row_shift<D>((int)(b & 0xffffffffLL)), hi = row_shift<D>((int)(b >> 32));
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+template <int D>
+__device__ __forceinline__ float row_shift(float x) {
+  return __int_as_float(row_shift<D>(__float_as_int(x)));
+}
 
+// DPP lane permutes within a row of 16 lanes (VALU modifiers: no LDS round
+// trip, unlike the bpermute behind __shfl_xor).
+template <int CTRL>
+__device__ __forceinline__ int dpp(int x) { return __builtin_amdgcn_update_dpp(0, x, CTRL, 0xf, 0xf, false); }
+template <int CTRL>
+__device__ __forceinline__ double dpp(double x) {
+  const long long b = __double_as_longlong(x);
+  const int lo = dpp<CTRL>((int)(b & 0xffffffffLL)), hi = dpp<CTRL>((int)(b >> 32));
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+template <int CTRL>
+__device__ __forceinline__ float dpp(float x) { return __int_as_float(dpp<CTRL>(__float_as_int(x))); }
+constexpr int kDppXor1 = 0xB1;         // quad_perm [1,0,3,2]
+constexpr int kDppXor2 = 0x4E;         // quad_perm [2,3,0,1]
+constexpr int kDppHalfMirror = 0x141;  // lane i <-> 7-i within each half row
+constexpr int kDppMirror = 0x140;      // lane i <-> 15-i within each row
+
+// Sum over the wave, returned wave-uniform: a DPP butterfly inside each row
+// of 16 lanes (xor 1, xor 2, half mirror, mirror: every lane then holds its
+// row's sum), then the four row sums by readlane.  Call with every lane
+// active (lanes without data contribute 0).
 template <typename R>
 __device__ __forceinline__ R wave_sum(R x) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
-  return x;
+  x += dpp<kDppXor1>(x);
+  x += dpp<kDppXor2>(x);
+  x += dpp<kDppHalfMirror>(x);
+  x += dpp<kDppMirror>(x);
+  return (rdlane(x, 0) + rdlane(x, 16)) + (rdlane(x, 32) + rdlane(x, 48));
 }
 
 template <typename R>
@@ -47,14 +89,22 @@ __device__ __forceinline__ void argmin_combine(R& v, int& i, R v2, int i2) {
   if (v2 < v || (v2 == v && i2 < i)) { v = v2; i = i2; }
 }
 
+// (min v, its smallest i) over the wave, wave-uniform; the same row butterfly
+// + readlane shape as wave_sum.  Lexicographic (v, i) minimum: independent of
+// the combining order.
 template <typename R>
 __device__ __forceinline__ void wave_argmin(R& v, int& i) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    R v2 = __shfl_xor(v, o, 64);
-    int i2 = __shfl_xor(i, o, 64);
-    argmin_combine(v, i, v2, i2);
-  }
+  argmin_combine(v, i, dpp<kDppXor1>(v), dpp<kDppXor1>(i));
+  argmin_combine(v, i, dpp<kDppXor2>(v), dpp<kDppXor2>(i));
+  argmin_combine(v, i, dpp<kDppHalfMirror>(v), dpp<kDppHalfMirror>(i));
+  argmin_combine(v, i, dpp<kDppMirror>(v), dpp<kDppMirror>(i));
+  R vb = rdlane(v, 0);
+  int ib = __builtin_amdgcn_readlane(i, 0);
+  argmin_combine(vb, ib, rdlane(v, 16), __builtin_amdgcn_readlane(i, 16));
+  argmin_combine(vb, ib, rdlane(v, 32), __builtin_amdgcn_readlane(i, 32));
+  argmin_combine(vb, ib, rdlane(v, 48), __builtin_amdgcn_readlane(i, 48));
+  v = vb;
+  i = ib;
 }
 
 // S_t storage order (22 entries):
@@ -103,12 +153,12 @@ __device__ __forceinline__ void adt_times(R (&g)[12], R dt, R cp, R sp) {
 }
 
 // The same two maps lane-parallel: lane r < 12 holds component r.  The
-// cross terms come from other lanes (readlane / bpermute); lanes >= 12 pass
+// cross terms come from other lanes (readlane / DPP row shift); lanes >= 12 pass
 // their value through unchanged.
 template <typename R>
 __device__ __forceinline__ R ad_lane(R x, R dt, R cp, R sp) {
   const int r = threadIdx.x;
-  const R xv = __shfl(x, (int)((threadIdx.x + 6) & 63), 64);   // x[r+6] for r < 3
+  const R xv = row_shift<6>(x);   // x[r+6] for r < 3
   const R w0 = rdlane(x, 9), w1 = rdlane(x, 10), w2 = rdlane(x, 11);
   R d = R(0);
   d = (r < 3) ? xv : d;
@@ -120,7 +170,7 @@ __device__ __forceinline__ R ad_lane(R x, R dt, R cp, R sp) {
 template <typename R>
 __device__ __forceinline__ R adt_lane(R g, R dt, R cp, R sp) {
   const int r = threadIdx.x;
-  const R gv = __shfl(g, (int)((threadIdx.x + 58) & 63), 64);  // g[r-6] for 6 <= r < 9
+  const R gv = row_shift<-6>(g);  // g[r-6] for 6 <= r < 9
   const R g3 = rdlane(g, 3), g4 = rdlane(g, 4), g5 = rdlane(g, 5);
   R d = R(0);
   d = (r >= 6 && r < 9) ? gv : d;
