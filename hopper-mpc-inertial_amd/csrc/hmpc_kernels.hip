@@ -260,6 +260,14 @@ struct Lay {
 
 __device__ __forceinline__ int loff(int r) { return (r * (r + 1)) >> 1; }
 
+// prefetch depth (steps) of the two-wave sweeps' LDS ring (two loads a step:
+// lgkmcnt waits of 2 kRing2 - 2 <= 15)
+#ifndef HMPC_RING2
+#define HMPC_RING2 8
+#endif
+constexpr int kRing2 = HMPC_RING2;
+static_assert(kRing2 == 4 || kRing2 == 8, "ring depth");
+
 // ----------------------------------------------------------------------------
 // triangular sweeps.  The factor is kept as the unit lower M = L diag(L)^-1:
 // row tid of M in lane tid's registers (Mr, after the Cholesky), and a
@@ -322,7 +330,7 @@ __device__ __forceinline__ double tri_fwd_lds(double acc, const double* Mc, cons
                                               double dinv, double* red, int s0 = 0) {
   using L = Lay<N>;
   constexpr int NV = L::NV;
-  constexpr int SEND = (NV + 3) & ~3;   // padded (steps >= NV are no-ops)
+  constexpr int SEND = L::W == 1 ? (NV + 3) & ~3 : ((NV + kRing2 - 1) / kRing2) * kRing2;   // padded (steps >= NV are no-ops)
   const int tid = threadIdx.x;
   if constexpr (L::W == 1) {
     // M[tid][s] for tid > s sits at Mc[cb(s) + tid - s]; other lanes read a 0
@@ -361,28 +369,29 @@ __device__ __forceinline__ double tri_fwd_lds(double acc, const double* Mc, cons
     auto ad1 = [&](int s) -> unsigned {
       return (lane + 64 > s && lane + 64 < NV && s < NV) ? b1 + 8u * (unsigned)(L::cb(s) - s) : zaddr;
     };
-    double r0[4], r1[4];
-    sfor<0, 4>([&](auto jc) __attribute__((always_inline)) {
+    constexpr int RD = kRing2;   // s0 is a multiple of RD here
+    double r0[RD], r1[RD];
+    sfor<0, RD>([&](auto jc) __attribute__((always_inline)) {
       constexpr int j = decltype(jc)::value;
       lds_ld64(r0[j], ad0(s0 + j));
       lds_ld64(r1[j], ad1(s0 + j));
     });
     auto steps = [&](int s, const double& src, int off) __attribute__((always_inline)) {
-      sfor<0, 4>([&](auto jc) __attribute__((always_inline)) {
+      sfor<0, RD>([&](auto jc) __attribute__((always_inline)) {
         constexpr int j = decltype(jc)::value;
         const int sj = s + j;
         const double ys = rdlane(src, sj - off);
-        lds_wait<6>(r0[j], r1[j]);
+        lds_wait<2 * RD - 2>(r0[j], r1[j]);
         a0 = fma(-r0[j], ys, a0);
         a1 = fma(-r1[j], ys, a1);
-        lds_ld64(r0[j], ad0(sj + 4));
-        lds_ld64(r1[j], ad1(sj + 4));
+        lds_ld64(r0[j], ad0(sj + RD));
+        lds_ld64(r1[j], ad1(sj + RD));
       });
     };
 #pragma unroll 1
-    for (int s = s0; s < 64; s += 4) steps(s, a0, 0);
+    for (int s = s0; s < 64; s += RD) steps(s, a0, 0);
 #pragma unroll 1
-    for (int s = (s0 > 64 ? s0 : 64); s < SEND; s += 4) steps(s, a1, 64);
+    for (int s = (s0 > 64 ? s0 : 64); s < SEND; s += RD) steps(s, a1, 64);
     lds_wait<0>(r0[0], r1[0]);   // drain the ring (its last loads are dummies)
     acc = tid < 64 ? a0 : a1;
   }
@@ -435,28 +444,30 @@ __device__ __forceinline__ double tri_bwd(double acc, const double* Mc, const do
     auto ad1 = [&](int s) -> unsigned {
       return (lane + 64 < s && s < NV && s >= 0) ? b1 + 8u * (unsigned)s : zaddr;
     };
-    double r0[4], r1[4];
-    sfor<0, 4>([&](auto jc) __attribute__((always_inline)) {
+    constexpr int RD = kRing2;
+    constexpr int STOP2 = ((NV + RD - 1) / RD) * RD - 1;   // first step, padded to the ring
+    double r0[RD], r1[RD];
+    sfor<0, RD>([&](auto jc) __attribute__((always_inline)) {
       constexpr int j = decltype(jc)::value;
-      lds_ld64(r0[j], ad0(STOP - j));
-      lds_ld64(r1[j], ad1(STOP - j));
+      lds_ld64(r0[j], ad0(STOP2 - j));
+      lds_ld64(r1[j], ad1(STOP2 - j));
     });
     auto steps = [&](int s, const double& src, int off) __attribute__((always_inline)) {
-      sfor<0, 4>([&](auto jc) __attribute__((always_inline)) {
+      sfor<0, RD>([&](auto jc) __attribute__((always_inline)) {
         constexpr int j = decltype(jc)::value;
         const int sj = s - j;
         const double zs = rdlane(src, sj - off);
-        lds_wait<6>(r0[j], r1[j]);
+        lds_wait<2 * RD - 2>(r0[j], r1[j]);
         a0 = fma(-r0[j], zs, a0);
         a1 = fma(-r1[j], zs, a1);
-        lds_ld64(r0[j], ad0(sj - 4));
-        lds_ld64(r1[j], ad1(sj - 4));
+        lds_ld64(r0[j], ad0(sj - RD));
+        lds_ld64(r1[j], ad1(sj - RD));
       });
     };
 #pragma unroll 1
-    for (int s = STOP; s >= 64; s -= 4) steps(s, a1, 64);
+    for (int s = STOP2; s >= 64; s -= RD) steps(s, a1, 64);
 #pragma unroll 1
-    for (int s = 63; s >= 0; s -= 4) steps(s, a0, 0);
+    for (int s = 63; s >= 0; s -= RD) steps(s, a0, 0);
     lds_wait<0>(r0[0], r1[0]);
     acc = tid < 64 ? a0 : a1;
   }
@@ -1174,7 +1185,7 @@ solve_kernel(SolveArgs a) {
     // w = L^-1 n_p
     HMPC_TIC(t_fwd);
     const int s0 = B::first(np_me != 0.0, red);   // first nonzero of n_p (-1: none)
-    const double wfull = tri_fwd_lds<N>(np_me, Lc, zero, dinv, xs, s0 > 0 ? (s0 & ~3) : 0);
+    const double wfull = tri_fwd_lds<N>(np_me, Lc, zero, dinv, xs, s0 > 0 ? (s0 & ~(W == 1 ? 3 : kRing2 - 1)) : 0);
     const double wnorm2 = B::sum(wfull * wfull, red);
     HMPC_TOC(10, t_fwd);
 
