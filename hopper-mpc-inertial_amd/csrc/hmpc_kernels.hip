@@ -772,30 +772,29 @@ solve_kernel(SolveArgs a) {
   {
     const int ii = active_lane ? vj3 : 0;
     const int ci = active_lane ? vc3 : 0;
-    // my impulse b = Bd_i e_c (rows 6..11) and f = S_{i+1} b
+    // my impulse b = Bd_i e_c (rows 6..11) and f = S_{i+1} b; zero for fixed
+    // variables and idle lanes, whose rows of H are then zero (their unit
+    // diagonal is added at the pivot, as is every 2 V_i: phase 4)
+    const double rowm = (active_lane && !my_fixed) ? 1.0 : 0.0;
     const double cpi = sm[L::CS + 2 * ii], spi = sm[L::CS + 2 * ii + 1];
     const double* bwi = sm + L::BW + 18 * ii;
     double e0[12], f[12];
 #pragma unroll
     for (int r = 0; r < 6; ++r) e0[r] = 0.0;
 #pragma unroll
-    for (int r = 0; r < 3; ++r) e0[6 + r] = ci < 3 ? bv<VAR>(r, ci, dtm, cpi, spi) : 0.0;
+    for (int r = 0; r < 3; ++r) e0[6 + r] = ci < 3 ? rowm * bv<VAR>(r, ci, dtm, cpi, spi) : 0.0;
 #pragma unroll
-    for (int r = 0; r < 3; ++r) e0[9 + r] = bwi[6 * r + ci];
+    for (int r = 0; r < 3; ++r) e0[9 + r] = rowm * bwi[6 * r + ci];
     s_times(sm + L::SS + 22 * ii, e0, f);
-    // diagonal block H[v, (i, c2)] = 2 Bd_i[:,c2]' S_{i+1} Bd_i e_c + 2 V_i
-    double hd[6];
-#pragma unroll
-    for (int c2 = 0; c2 < 6; ++c2) {
-      hd[c2] = bd_dot<VAR>(c2, f, bwi, dtm, cpi, spi);
-      if (c2 == ci && ii != N - 1) hd[c2] += 2.0 * kRdiag;
-    }
     // gradient: h_v = 2 b' a_{i+1} (b = Bd_i e_c, a = adjoint of phase 2)
     double hacc = 0.0;
 #pragma unroll
     for (int r = 0; r < 6; ++r) hacc = fma(e0[6 + r], sm[L::AJ + 6 * ii + r], hacc);
-    // lower part, j < i: H[v, (j, c2)] = 2 Bd_j[:,c2]' g_j,
-    // g_i = f, g_j = Ad_{j+1}' g_{j+1}
+    // H[v, (j, c2)] = 2 Bd_j[:,c2]' g_j with g_i = f, g_j = Ad_{j+1}' g_{j+1}
+    // (j < i).  Only the lower triangle is ever read (the Cholesky publishes
+    // column k from lanes >= k and overwrites register k), so entries right
+    // of the diagonal keep whatever finite value falls out; the diagonal
+    // block needs no special case (its 2 V_i goes in at the pivot).
     double g[12];
 #pragma unroll
     for (int r = 0; r < 12; ++r) g[r] = f[r];
@@ -813,17 +812,15 @@ solve_kernel(SolveArgs a) {
       }
       const double cp = smj[L::CS + 2 * j], sp = smj[L::CS + 2 * j + 1];
       const double* bw = smj + L::BW + 18 * j;
-      const bool stance_j = smj[L::CC + j] != 0.0;
+      // fixed columns (swing forces :134-136) of stage j: zero
+      const double stance_j = smj[L::CC + j] != 0.0 ? 1.0 : 0.0;
       sfor<0, 6>([&](auto c2c) __attribute__((always_inline)) {
         constexpr int c2 = decltype(c2c)::value;
         constexpr int w = 6 * j + c2;
-        const double lo = bd_dot<VAR>(c2, g, bw, dtm, cp, sp);
-        double val = (ii > j) ? lo : ((ii == j && c2 <= ci) ? hd[c2] : 0.0);
-        // fixed variables: their row and column of H are those of the identity
-        const bool colfix = (c2 < 3 && !stance_j) || (VAR == 2 && c2 == 1);
-        if (colfix || my_fixed) val = 0.0;
-        if (my_fixed && w == tid) val = 1.0;
-        if (!active_lane) val = 0.0;
+        double val;
+        if constexpr (VAR == 2 && c2 == 1) val = 0.0;   // 2f fy (2f :129)
+        else if constexpr (c2 < 3) val = stance_j * bd_dot<VAR>(c2, g, bw, dtm, cp, sp);
+        else val = bd_dot<VAR>(c2, g, bw, dtm, cp, sp);
         Rg[w] = val;
         pin(Rg[w]);
       });
@@ -841,6 +838,11 @@ solve_kernel(SolveArgs a) {
 
   int status = ST_SOLVED;
   double dinv = 0.0;
+  // the diagonal of H not built in phase 3: 1 for a fixed variable (identity
+  // row/column), else 2 V_i (R * kuf: every stage but the last, 3f :114,132,139)
+  auto diag_extra = [&](int k, bool fixed) -> double {
+    return fixed ? 1.0 : ((k / 6 != N - 1) ? 2.0 * kRdiag : 0.0);
+  };
 
   // ---------------- phase 4: Cholesky ---------------------------------------
   // Right-looking, lane v holds row v of the trailing matrix in registers
@@ -875,6 +877,7 @@ solve_kernel(SolveArgs a) {
                                          : ((NV - ja - CW * ch) > 0 ? (NV - ja - CW * ch + 1) / 2 : 0);
       };
       const uint64_t fixmask = __ballot(active_lane && is_fixed(vj3, vc3));
+      const double dx = diag_extra(tid, my_fixed);   // lane s: the extra of pivot s
       dbl2 nb[CW / 2];                 // chunk 0 of the next step
       double p_rs = 0.0, p_tk = 0.0;   // next step's 1/L_kk and M[tid][k]
       auto ahead = [&](auto sc) __attribute__((always_inline)) {
@@ -892,7 +895,7 @@ solve_kernel(SolveArgs a) {
           constexpr int i = decltype(ic)::value;
           lds_ld128<16 * i>(nb[i], cb0);
         });
-        const double piv = rdlane(mine, s);
+        const double piv = rdlane(mine + dx, s);
         const double pv = piv > 0.0 ? piv : 1.0;
         nbad += (piv > 0.0) ? 0.0 : 1.0;   // folded into status after the loop
         pin(nbad);                          // (materialised here, not sunk to the end)
@@ -977,6 +980,12 @@ solve_kernel(SolveArgs a) {
       });
     } else {
       double mine = Rg[0];   // A[tid][k] of the current step
+      // pivot extras (diag_extra) by lane, behind the column buffers (the
+      // active-set state there is not live yet); the first step's barrier
+      // publishes them
+      double* dxa = sm + L::COLB + 2 * (NT + 8);
+      static_assert(L::COLB + 2 * (NT + 8) + NT <= L::U0, "pivot extras do not fit");
+      dxa[tid] = diag_extra(tid, my_fixed);
       sfor<0, (NV + 7) / 8>([&](auto bc) __attribute__((always_inline)) {
         constexpr int bb = decltype(bc)::value;
         constexpr int J0 = 8 * bb;
@@ -987,7 +996,7 @@ solve_kernel(SolveArgs a) {
           double* col = sm + L::COLB + (k & 1) * (NT + 8);
           col[tid] = (tid >= k && tid < NV) ? mine : 0.0;
           B::sync();
-          const double piv = col[k];
+          const double piv = col[k] + dxa[k];
           const unsigned cbase = lds_addr(col + J0);
           dbl2 buf[2][4];
           auto load = [&](auto chc) __attribute__((always_inline)) {
