@@ -885,10 +885,11 @@ solve_kernel(SolveArgs a) {
         constexpr int JS = (s + 1) & ~1;
         // lane masks of a step come from an opaque copy of its index: hoisted
         // out of the unrolled steps they would pin ~100 SGPRs (and spill)
-        const int so = s + opaque_zero();
         double* col = sm + L::COLB + (s & 1) * (NT + 8);
         const double mine = Rg[s];
-        col[tid] = (tid >= so && tid < NV) ? mine : 0.0;
+        // unmasked: the updates read rows > s only (lanes < s hold
+        // don't-care upper-triangle values there, lanes >= NV are never read)
+        col[tid] = mine;
         B::sync();
         const unsigned cb0 = lds_addr(col + JS);
         sfor<0, nldc(JS, 0)>([&](auto ic) __attribute__((always_inline)) {
@@ -914,7 +915,9 @@ solve_kernel(SolveArgs a) {
         const double rs = p_rs, tk = p_tk;
         lds_wait<0>(nb[0], nb[1]);   // this step's chunk 0 (and everything older)
         const bool below = tid > ko && tid < NV;
-        const double nt = below ? -tk : 0.0;
+        // every lane updates: a lane <= k changes only its registers > k, the
+        // upper triangle of its row (don't-care, overwritten at their step)
+        const double nt = -tk;
         // branch-free store of column k of M (other lanes: the column buffer
         // of step k+1, which ahead() rewrites after this store)
         {
