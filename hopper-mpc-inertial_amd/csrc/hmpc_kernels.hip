@@ -1019,7 +1019,9 @@ solve_kernel(SolveArgs a) {
           const double tk = (mine * rs) * rs;
           const bool below = tid > k && tid < NV;
           const double mk = below ? tk : 0.0;
-          const double nt = below ? -tk : 0.0;
+          // unmasked: the published column is 0 above row k, so a lane <= k
+          // changes only its upper triangle (registers > k, never read)
+          const double nt = -tk;
           double nxt = 0.0;
           sfor<0, NCH>([&](auto chc) __attribute__((always_inline)) {
             constexpr int ch = decltype(chc)::value;
