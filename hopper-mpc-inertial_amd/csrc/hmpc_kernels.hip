@@ -687,21 +687,25 @@ solve_kernel(SolveArgs a) {
       for (int e = 0; e < 22; ++e) sm[L::SS + 22 * (N - 1) + e] = s[e];
     }
     // stage k's yaw cos/sin from lane k (readlane: no LDS round trip in the
-    // recursions' chains); the reference row is fetched one stage ahead
+    // recursions' chains).  Both loops are unrolled: the reference rows are
+    // loaded up front and the gradient terms d_t stay in registers (lane
+    // r < 12: component r), so no load sits inside a recursion.
     const double cpl = tid < N ? sm[L::CS + 2 * tid] : 0.0;
     const double spl = tid < N ? sm[L::CS + 2 * tid + 1] : 0.0;
-    double xrn = tid < 12 ? sm[L::XREF + tid] : 0.0;
-#pragma unroll 1
-    for (int k = 0; k < N; ++k) {
+    double xrf[N], dgv[N];
+    sfor<0, N>([&](auto kc) __attribute__((always_inline)) {
+      constexpr int k = decltype(kc)::value;
+      xrf[k] = sm[L::XREF + 12 * k + (tid < 12 ? tid : 0)];
+    });
+    sfor<0, N>([&](auto kc) __attribute__((always_inline)) {
+      constexpr int k = decltype(kc)::value;
       const double cp = rdlane(cpl, k), sp = rdlane(spl, k);
-      const double xrk = xrn;
-      xrn = (tid < 12 && k + 1 < N) ? sm[L::XREF + 12 * (k + 1) + tid] : 0.0;
       xr = ad_lane(xr, dt, cp, sp) + ((tid == 8) ? -a.g * dt : 0.0);
       const double kf = (k == N - 1) ? kTermQ : 1.0;
-      if (tid < 12) sm[L::DG + 12 * k + tid] = kf * qr * (xr - xrk);
+      dgv[k] = kf * qr * (xr - xrf[k]);   // 0 on lanes >= 12 (qr = 0)
       if (tid == 2) sm[L::ZB + k + 1] = xr;
-      const int t = N - 1 - k;
-      if (t >= 1) {
+      constexpr int t = N - 1 - k;
+      if constexpr (t >= 1) {
         const double ct = rdlane(cpl, t), st = rdlane(spl, t);
         // translational axes and yaw: [[a, b], [b, c]] with p' = p + dt v
 #pragma unroll
@@ -739,21 +743,18 @@ solve_kernel(SolveArgs a) {
 #pragma unroll
           for (int e = 0; e < 22; ++e) sm[L::SS + 22 * (t - 1) + e] = s[e];
       }
-    }
+    });
     B::sync();
     // adjoint a_N = d_N, a_t = d_t + Ad_t' a_{t+1} (lane-parallel): the
     // gradient of the tracking cost w.r.t. x_t.  Only rows 6..11 are kept
     // (the nonzero rows of Bd).
-    double ar = tid < 12 ? sm[L::DG + 12 * (N - 1) + tid] : 0.0;
+    double ar = dgv[N - 1];
     if (tid >= 6 && tid < 12) sm[L::AJ + 6 * (N - 1) + tid - 6] = ar;
-    double dgn = (tid < 12 && N >= 2) ? sm[L::DG + 12 * (N - 2) + tid] : 0.0;
-#pragma unroll 1
-    for (int t = N - 1; t >= 1; --t) {
-      const double dgt = dgn;
-      dgn = (tid < 12 && t >= 2) ? sm[L::DG + 12 * (t - 2) + tid] : 0.0;
-      ar = adt_lane(ar, dt, rdlane(cpl, t), rdlane(spl, t)) + dgt;
+    sfor<1, N>([&](auto ic) __attribute__((always_inline)) {
+      constexpr int t = N - decltype(ic)::value;   // N-1 .. 1
+      ar = adt_lane(ar, dt, rdlane(cpl, t), rdlane(spl, t)) + dgv[t - 1];
       if (tid >= 6 && tid < 12) sm[L::AJ + 6 * (t - 1) + tid - 6] = ar;
-    }
+    });
   }
   __syncthreads();
   HMPC_STAMP(3);
