@@ -1100,17 +1100,16 @@ solve_kernel(SolveArgs a) {
     if (vc >= 3) nslots = (vc == 3 && vj >= 2) ? 3 : 2;
     else if (stance_me && !(VAR == 2 && vc == 1)) nslots = 2;
   }
-  double znorm = 0.0;
-  if (active_lane && vc == 3 && vj >= 2) {
-    double s2 = 0.0;
-    for (int j = 0; j <= vj - 2; ++j) {
-      if (sm[L::CC + j] != 0.0) {
-        const double cz = zc * (double)(vj - 1 - j);
-        s2 += cz * cz;
-      }
-    }
-    znorm = sqrt(s2);
-  }
+  // |n| of my z row (stance stages j <= k-2): a uniform, unrolled masked sum
+  // (a per-lane loop would diverge and wait on one LDS load per trip)
+  double s2 = 0.0;
+  sfor<0, (N > 2 ? N - 2 : 0)>([&](auto jc) __attribute__((always_inline)) {
+    constexpr int j = decltype(jc)::value;
+    const double cz = zc * (double)(vj - 1 - j);
+    const double m = (j <= vj - 2 && sm[L::CC + j] != 0.0) ? 1.0 : 0.0;
+    s2 = fma(m * cz, cz, s2);
+  });
+  const double znorm = (active_lane && vc == 3 && vj >= 2) ? sqrt(s2) : 0.0;
   // slot 0/1 coefficients of my constraints (see the table above)
   double a0 = 1.0, muf = 0.0, k0 = 0.0, k1 = 0.0, inv01 = 1.0;
   if (vc >= 3) {
