@@ -269,9 +269,8 @@ constexpr int kRing2 = HMPC_RING2;
 static_assert(kRing2 == 4 || kRing2 == 8, "ring depth");
 
 // ----------------------------------------------------------------------------
-// triangular sweeps.  The factor is kept as the unit lower M = L diag(L)^-1:
-// row tid of M in lane tid's registers (Mr, after the Cholesky), and a
-// column-major packed copy in LDS with 1/L_kk in the (unit) diagonal slot of
+// triangular sweeps.  The factor is kept as the unit lower M = L diag(L)^-1,
+// column-major packed in LDS with 1/L_kk in the (unit) diagonal slot of
 // column k.  L^-1 b = diag(1/L) M^-1 b and L^-T b = M^-T (diag(1/L) b): one
 // step's dependent chain is just readlane -> fma.
 // ----------------------------------------------------------------------------
@@ -285,43 +284,10 @@ __device__ __forceinline__ void sweep_stage(double b, double& a0, double& a1, do
   a0 = buf[lane];
   a1 = buf[lane + 64];
 }
-// y = L^-1 b (lane v holds b_v), M from registers, fully unrolled.
-// Mr[s] = M[tid][s] below the diagonal and 0 on and above it.
-// The first NLDS columns come from the LDS copy instead (loaded up front):
-// their registers are then dead from the Cholesky step that finishes them,
-// which keeps the factorisation's live set inside the register file (they
-// were the ones spilled to scratch otherwise).
-template <int N, int NLDS = 0>
-__device__ __forceinline__ double tri_fwd(double acc, const double (&Mr)[6 * N], double dinv,
-                                          double* red, const double* Mc = nullptr,
-                                          const double* zero = nullptr) {
-  using L = Lay<N>;
-  constexpr int NV = L::NV;
-  const int tid = threadIdx.x;
-  (void)tid;
-  double ml[NLDS > 0 ? NLDS : 1];
-  if constexpr (NLDS > 0) {
-    sfor<0, NLDS>([&](auto sc) __attribute__((always_inline)) {
-      constexpr int s = decltype(sc)::value;
-      // M[tid][s] for tid > s sits at Mc[cb(s) + tid - s]; other lanes read a 0
-      lds_ld64(ml[s], lds_addr((tid > s && tid < NV) ? Mc + L::cb(s) + tid - s : zero));
-    });
-  }
-  sfor<0, NV>([&](auto sc) __attribute__((always_inline)) {
-    constexpr int s = decltype(sc)::value;
-    if constexpr (s < NLDS) {
-      lds_wait<NLDS - 1 - s>(ml[s]);
-      acc = fma(-ml[s], Blk<L::W>::bcast(acc, s, red), acc);
-    } else {
-      acc = fma(-Mr[s], Blk<L::W>::bcast(acc, s, red), acc);
-    }
-  });
-  // lane v's accumulator is final once step v has read it (M[v][s] = 0, s >= v)
-  return acc * dinv;
-}
-// The same sweep from the LDS copy (the active-set phase, where the
-// registers hold the Gram-Schmidt basis instead): loads of step s+4 are
-// issued at step s (a 4-deep ring of hand-counted loads).  s0 (uniform, a
+// y = L^-1 b (lane v holds b_v) from the LDS copy of M (the one-wave
+// kernel's phase-5 forward sweep instead rides along the Cholesky).  Loads
+// of step s+4 are issued at step s (a 4-deep ring of hand-counted loads).
+// s0 (uniform, a
 // multiple of 4): b is zero above row s0, so are the first s0 entries of y
 // and the sweep starts there (constraint normals are sparse: a box or
 // friction row of stage j starts at 6j).
@@ -495,10 +461,6 @@ __device__ __forceinline__ double tri_bwd(double acc, const double* Mc, const do
 #define HMPC_TOC(slot, v) ((void)0)
 #endif
 
-// columns of the phase-5 forward sweep read from LDS (tri_fwd)
-#ifndef HMPC_FWD_NLDS
-#define HMPC_FWD_NLDS 8
-#endif
 #ifndef HMPC_WAVES_PER_EU
 #define HMPC_WAVES_PER_EU(W) ((W) == 1 ? 2 : 1)
 #endif
@@ -833,7 +795,8 @@ solve_kernel(SolveArgs a) {
       hv = 2.0 * hacc - 2.0 * Vj * ub;
     }
   }
-  xs[tid] = hv;      // parked in LDS across the factorisation
+  xs[tid] = hv;      // parked in LDS across the factorisation (two waves)
+  double wv = -hv;   // one wave: the forward sweep's accumulator (phase 4)
   __syncthreads();   // union A (XLIN/XREF/PF/S/DG) is dead from here on
   HMPC_STAMP(4);
 
@@ -848,12 +811,13 @@ solve_kernel(SolveArgs a) {
   // ---------------- phase 4: Cholesky ---------------------------------------
   // Right-looking, lane v holds row v of the trailing matrix in registers
   // (register j = column j).  Step k publishes column k (lanes >= k) through
-  // LDS; every lane then updates its registers j > k.  Afterwards register k
-  // holds M[tid][k] = L[tid][k] / L[k][k] below the diagonal (0 elsewhere):
-  // the row IS row tid of M, which the forward sweep reads from registers.
-  // A column-major copy of M (1/L_kk on the diagonal) goes to LDS for the
-  // backward sweeps.  Column loads are issued before the pivot arithmetic
-  // (hand-counted waits).
+  // LDS; every lane then updates its registers j > k.  Step k's multipliers
+  // M[i][k] = L[i][k] / L[k][k] go column-major to LDS (1/L_kk on the
+  // diagonal) for the sweeps; one wave also runs phase 5's forward
+  // substitution inside the steps.  Column loads are issued before the pivot
+  // arithmetic (hand-counted waits).  Only the lower triangle of the
+  // registers is meaningful; the diagonal's 2 V_i (or a fixed variable's 1)
+  // is added to the pivot (diag_extra).
   //   NV <= 64 (one wave): every step unrolled -- no runtime index, no selects.
   //   NV >  64: blocks of 8 steps share one runtime loop body (code size).
   {
@@ -926,7 +890,9 @@ solve_kernel(SolveArgs a) {
           const int o_d = L::COLB + ((k + 1) & 1) * (NT + 8) + tid;
           sm[(tid >= ko && tid < NV) ? o_l : o_d] = (tid == ko) ? rs : tk;
         }
-        Rg[k] = below ? tk : 0.0;
+        // phase 5's forward substitution w = M^-1 (-h) rides along: w_k is
+        // final here, rows below take -M[i][k] w_k (off the step's chain)
+        wv = fma(below ? -tk : 0.0, rdlane(wv, k), wv);
         const unsigned cbase = lds_addr(sm + L::COLB + (k & 1) * (NT + 8) + JA);
         // chunks >= 1 go through a 3-deep ring: chunk ch+2 is issued while
         // chunk ch is consumed (one chunk ahead left the LDS latency exposed)
@@ -1063,7 +1029,7 @@ solve_kernel(SolveArgs a) {
   double v = 0.0;
   {
     double y;
-    if constexpr (W == 1) y = tri_fwd<N, HMPC_FWD_NLDS>(-xs[tid], Rg, dinv, red, Lc, zero);
+    if constexpr (W == 1) y = wv * dinv;   // L^-1 (-h), swept during the Cholesky
     else y = tri_fwd_lds<N>(-xs[tid], Lc, zero, dinv, xs);   // no per-step exchange
     v = tri_bwd<N>(y, Lc, zero, dinv, xs);
   }
