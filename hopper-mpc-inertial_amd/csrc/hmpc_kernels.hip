@@ -795,8 +795,7 @@ solve_kernel(SolveArgs a) {
       hv = 2.0 * hacc - 2.0 * Vj * ub;
     }
   }
-  xs[tid] = hv;      // parked in LDS across the factorisation (two waves)
-  double wv = -hv;   // one wave: the forward sweep's accumulator (phase 4)
+  double wv = -hv;   // the forward sweep's accumulator (phase 4)
   __syncthreads();   // union A (XLIN/XREF/PF/S/DG) is dead from here on
   HMPC_STAMP(4);
 
@@ -813,8 +812,8 @@ solve_kernel(SolveArgs a) {
   // (register j = column j).  Step k publishes column k (lanes >= k) through
   // LDS; every lane then updates its registers j > k.  Step k's multipliers
   // M[i][k] = L[i][k] / L[k][k] go column-major to LDS (1/L_kk on the
-  // diagonal) for the sweeps; one wave also runs phase 5's forward
-  // substitution inside the steps.  Column loads are issued before the pivot
+  // diagonal) for the sweeps; phase 5's forward substitution runs inside
+  // the steps.  Column loads are issued before the pivot
   // arithmetic (hand-counted waits).  Only the lower triangle of the
   // registers is meaningful; the diagonal's 2 V_i (or a fixed variable's 1)
   // is added to the pivot (diag_extra).
@@ -965,8 +964,10 @@ solve_kernel(SolveArgs a) {
         for (int k = J0; k < KEND; ++k) {
           double* col = sm + L::COLB + (k & 1) * (NT + 8);
           col[tid] = (tid >= k && tid < NV) ? mine : 0.0;
+          if (tid == k) col[NT] = wv;   // w_k (final) for the riding forward sweep
           B::sync();
           const double piv = col[k] + dxa[k];
+          const double wk = col[NT];
           const unsigned cbase = lds_addr(col + J0);
           dbl2 buf[2][4];
           auto load = [&](auto chc) __attribute__((always_inline)) {
@@ -986,6 +987,7 @@ solve_kernel(SolveArgs a) {
           const double tk = (mine * rs) * rs;
           const bool below = tid > k && tid < NV;
           const double mk = below ? tk : 0.0;
+          wv = fma(-mk, wk, wv);   // phase 5's forward substitution (as one wave)
           // unmasked: the published column is 0 above row k, so a lane <= k
           // changes only its upper triangle (registers > k, never read)
           const double nt = -tk;
@@ -1029,8 +1031,7 @@ solve_kernel(SolveArgs a) {
   double v = 0.0;
   {
     double y;
-    if constexpr (W == 1) y = wv * dinv;   // L^-1 (-h), swept during the Cholesky
-    else y = tri_fwd_lds<N>(-xs[tid], Lc, zero, dinv, xs);   // no per-step exchange
+    y = wv * dinv;   // L^-1 (-h), swept during the Cholesky
     v = tri_bwd<N>(y, Lc, zero, dinv, xs);
   }
   HMPC_STAMP(6);
