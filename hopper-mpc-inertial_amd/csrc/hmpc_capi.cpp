@@ -33,6 +33,11 @@ struct hmpc_ctx {
   // generic-horizon kernel workspace (hmpc_wide.hip)
   double* wsbuf = nullptr;
   int wsgroups = 0;
+  // active-set overflow pass (hmpc_ric.hip): [count | list of ovf_cap ids]
+  // and the global R blocks of its workgroups
+  int32_t* ovf = nullptr;
+  int64_t ovf_cap = 0;
+  double* rws = nullptr;
   hipStream_t own_stream = nullptr;
 };
 
@@ -77,7 +82,7 @@ constexpr int kMaxGroups = 512;
 constexpr size_t kWsBudget = (size_t)4 << 30;   // bytes
 
 int prepare_ws(hmpc_ctx* c, int64_t B, hmpc::SolveArgs& a) {
-  if (c->precision == HMPC_PREC_F64 && hmpc::horizon_compiled(c->variant, c->N)) return HMPC_OK;
+  if (hmpc::pick_kernel(c->variant, c->N, c->precision) != hmpc::Kernel::Wide) return HMPC_OK;
   const hmpc::WideLayout Lw(c->N);
   const size_t per = (size_t)Lw.total * sizeof(double);
   int64_t want = B < kMaxGroups ? B : kMaxGroups;
@@ -98,6 +103,60 @@ int prepare_ws(hmpc_ctx* c, int64_t B, hmpc::SolveArgs& a) {
   a.ws = c->wsbuf;
   a.ws_stride = Lw.total;
   a.ws_groups = c->wsgroups;
+  return HMPC_OK;
+}
+
+// Overflow pass geometry: workgroups (each with an R block of capacity 6N in
+// global memory) looping over the instances whose active set outgrew the
+// main kernel's capacity.
+constexpr int kOvfGroups = 128;
+
+int prepare_ovf(hmpc_ctx* c, int64_t B, hmpc::SolveArgs& a) {
+  const hmpc::Kernel k = hmpc::pick_kernel(c->variant, c->N, c->precision);
+  a.ovf_count = nullptr; a.ovf_list = nullptr; a.rws = nullptr; a.rws_stride = 0;
+  if ((k != hmpc::Kernel::Dense && k != hmpc::Kernel::Riccati) || c->N > hmpc::kRicNmax) return HMPC_OK;
+  const int64_t nv = 6 * (int64_t)c->N;
+  const int64_t stride = ((nv * (nv + 1) / 2) + 15) & ~(int64_t)15;
+  if (!c->rws) {
+    hipError_t e = hipMalloc(&c->rws, sizeof(double) * stride * kOvfGroups);
+    if (e != hipSuccess) { c->rws = nullptr; c->err = "overflow workspace hipMalloc"; return HMPC_ERR_NOMEM; }
+  }
+  if (B > c->ovf_cap) {
+    if (c->ovf) (void)hipFree(c->ovf);
+    c->ovf = nullptr;
+    c->ovf_cap = 0;
+    hipError_t e = hipMalloc(&c->ovf, sizeof(int32_t) * (size_t)(B + 4));
+    if (e != hipSuccess) { c->err = "overflow list hipMalloc"; return HMPC_ERR_NOMEM; }
+    c->ovf_cap = B;
+  }
+  a.ovf_count = c->ovf;
+  a.ovf_list = c->ovf + 4;
+  a.rws = c->rws;
+  a.rws_stride = stride;
+  return HMPC_OK;
+}
+
+// One solve pass over the batch: the main kernel, then (dense / Riccati
+// kernels) the overflow pass over the instances it handed on.  Stream-ordered.
+int run_solve(hmpc_ctx* c, hmpc::SolveArgs a, hipStream_t s) {
+  int rc = prepare_ws(c, a.B, a);
+  if (rc != HMPC_OK) return rc;
+  rc = prepare_ovf(c, a.B, a);
+  if (rc != HMPC_OK) return rc;
+  if (a.ovf_count) {
+    hipError_t e = hipMemsetAsync(a.ovf_count, 0, sizeof(int32_t), s);
+    if (e != hipSuccess) return fail_hip(c, e, "hipMemsetAsync(overflow count)");
+  }
+  if (!hmpc::launch_solve(c->variant, c->N, a, s)) {
+    c->err = "no kernel for this (variant, N, precision)";
+    return HMPC_ERR_UNSUPPORTED;
+  }
+  if (a.ovf_count && !hmpc::launch_solve_ric_overflow(c->variant, c->N, a, kOvfGroups, s)) {
+    c->err = "overflow pass launch";
+    return HMPC_ERR_UNSUPPORTED;
+  }
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail_hip(c, e, "solve launch");
   return HMPC_OK;
 }
 
@@ -160,6 +219,8 @@ int hmpc_destroy(hmpc_ctx* c) {
   if (c->dbuf) (void)hipFree(c->dbuf);
   if (c->scratch_i32) (void)hipFree(c->scratch_i32);
   if (c->wsbuf) (void)hipFree(c->wsbuf);
+  if (c->ovf) (void)hipFree(c->ovf);
+  if (c->rws) (void)hipFree(c->rws);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   delete c;
   return HMPC_OK;
@@ -169,9 +230,14 @@ const char* hmpc_last_error(hmpc_ctx* c) { return c ? c->err.c_str() : ""; }
 
 int hmpc_set_precision(hmpc_ctx* c, int precision) {
   if (!c) return HMPC_ERR_ARG;
-  if (precision != HMPC_PREC_F64 && precision != HMPC_PREC_F32 && precision != HMPC_PREC_F64_GENERIC) {
+  if (precision != HMPC_PREC_F64 && precision != HMPC_PREC_F32 && precision != HMPC_PREC_F64_GENERIC &&
+      precision != HMPC_PREC_F64_RICCATI) {
     c->err = "unknown precision";
     return HMPC_ERR_ARG;
+  }
+  if (hmpc::pick_kernel(c->variant, c->N, precision) == hmpc::Kernel::None) {
+    c->err = "no kernel for this (variant, N) at that precision";
+    return HMPC_ERR_UNSUPPORTED;
   }
   c->precision = precision;
   return HMPC_OK;
@@ -185,11 +251,7 @@ int hmpc_solve_batch(hmpc_ctx* c, int64_t B, const double* x_in, const double* x
   if (rc != HMPC_OK || B == 0) return rc;
   HMPC_HIP(c, hipSetDevice(c->device));
   hmpc::SolveArgs a = make_args(c, B, x_in, x_lin, x_ref, pf, C, mu, u, x, obj, status, iters, 0);
-  rc = prepare_ws(c, B, a);
-  if (rc != HMPC_OK) return rc;
-  if (!hmpc::launch_solve(c->variant, c->N, a, (hipStream_t)stream)) return HMPC_ERR_UNSUPPORTED;
-  HMPC_HIP(c, hipGetLastError());
-  return HMPC_OK;
+  return run_solve(c, a, (hipStream_t)stream);
 }
 
 int hmpc_time_solve_batch(hmpc_ctx* c, int64_t B, const double* x_in, const double* x_lin,
@@ -198,25 +260,28 @@ int hmpc_time_solve_batch(hmpc_ctx* c, int64_t B, const double* x_in, const doub
                           int32_t* iters, int reps, void* stream, double* ms) {
   int rc = check_solve_args(c, B, x_in, x_lin, x_ref, pf, C, u, status);
   if (rc != HMPC_OK) return rc;
-  if (reps <= 0 || !ms || B == 0) return HMPC_ERR_ARG;
+  if (reps <= 0 || !ms || B == 0) { c->err = "reps <= 0, ms == NULL or B == 0"; return HMPC_ERR_ARG; }
   HMPC_HIP(c, hipSetDevice(c->device));
   hipStream_t s = (hipStream_t)stream;
-  hipEvent_t e0, e1;
-  HMPC_HIP(c, hipEventCreate(&e0));
-  HMPC_HIP(c, hipEventCreate(&e1));
   hmpc::SolveArgs a = make_args(c, B, x_in, x_lin, x_ref, pf, C, mu, u, x, obj, status, iters, 0);
-  rc = prepare_ws(c, B, a);
+  rc = run_solve(c, a, s);   // validates the combination and sizes the workspaces
   if (rc != HMPC_OK) return rc;
-  HMPC_HIP(c, hipEventRecord(e0, s));
-  for (int r = 0; r < reps; ++r) hmpc::launch_solve(c->variant, c->N, a, s);
-  HMPC_HIP(c, hipEventRecord(e1, s));
-  HMPC_HIP(c, hipEventSynchronize(e1));
+  struct Ev {   // destroyed on every exit path
+    hipEvent_t e = nullptr;
+    ~Ev() { if (e) (void)hipEventDestroy(e); }
+  } e0, e1;
+  HMPC_HIP(c, hipEventCreate(&e0.e));
+  HMPC_HIP(c, hipEventCreate(&e1.e));
+  HMPC_HIP(c, hipEventRecord(e0.e, s));
+  for (int r = 0; r < reps; ++r) {
+    rc = run_solve(c, a, s);
+    if (rc != HMPC_OK) return rc;
+  }
+  HMPC_HIP(c, hipEventRecord(e1.e, s));
+  HMPC_HIP(c, hipEventSynchronize(e1.e));
   float t = 0.f;
-  HMPC_HIP(c, hipEventElapsedTime(&t, e0, e1));
-  (void)hipEventDestroy(e0);
-  (void)hipEventDestroy(e1);
+  HMPC_HIP(c, hipEventElapsedTime(&t, e0.e, e1.e));
   *ms = (double)t / reps;
-  HMPC_HIP(c, hipGetLastError());
   return HMPC_OK;
 }
 
@@ -240,6 +305,10 @@ int hmpc_solve_batch_host(hmpc_ctx* c, int64_t B, const double* x_in, const doub
   }
   if (!c->own_stream) HMPC_HIP(c, hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking));
   hipStream_t s = c->own_stream;
+  // the context's workspaces are shared with the device entry points, which
+  // run on the caller's streams: drain the device first (this entry point is
+  // synchronous anyway)
+  HMPC_HIP(c, hipDeviceSynchronize());
   double* p = (double*)c->dbuf;
   double* d_xin = p; p += B * 12;
   double* d_xlin = p; p += B * 12 * (N + 1);
@@ -260,10 +329,8 @@ int hmpc_solve_batch_host(hmpc_ctx* c, int64_t B, const double* x_in, const doub
   if (mu) HMPC_HIP(c, hipMemcpyAsync(d_mu, mu, 8 * B, hipMemcpyHostToDevice, s));
   hmpc::SolveArgs a = make_args(c, B, d_xin, d_xlin, d_xref, d_pf, d_C, mu ? d_mu : nullptr,
                                 d_u, d_x, d_obj, d_st, d_it, 0);
-  rc = prepare_ws(c, B, a);
+  rc = run_solve(c, a, s);
   if (rc != HMPC_OK) return rc;
-  if (!hmpc::launch_solve(c->variant, c->N, a, s)) return HMPC_ERR_UNSUPPORTED;
-  HMPC_HIP(c, hipGetLastError());
   HMPC_HIP(c, hipMemcpyAsync(u, d_u, 8 * B * 6 * N, hipMemcpyDeviceToHost, s));
   if (x) HMPC_HIP(c, hipMemcpyAsync(x, d_x, 8 * B * 12 * (N + 1), hipMemcpyDeviceToHost, s));
   if (obj) HMPC_HIP(c, hipMemcpyAsync(obj, d_obj, 8 * B, hipMemcpyDeviceToHost, s));
@@ -283,12 +350,6 @@ int mpcontrol_impl(hmpc_ctx* c, int64_t B, int init, const double* x_in, const d
                    const hmpc::SolveArgs* view) {
   HMPC_HIP(c, hipSetDevice(c->device));
   hipStream_t s = (hipStream_t)stream;
-  {
-    hmpc::SolveArgs probe = make_args(c, B, x_in, x_prev, x_ref, pf, C, mu, u, x_prev, obj, status,
-                                      iters, 0);
-    const int rc = prepare_ws(c, B, probe);
-    if (rc != HMPC_OK) return rc;
-  }
   auto args = [&](int32_t* st, int32_t* it, double* ob, int mode) {
     hmpc::SolveArgs a = make_args(c, B, x_in, x_prev, x_ref, pf, C, mu, u, x_prev, ob, st, it, mode);
     if (view) {
@@ -296,9 +357,9 @@ int mpcontrol_impl(hmpc_ctx* c, int64_t B, int init, const double* x_in, const d
       a.pf_bs = view->pf_bs; a.pf_rs = view->pf_rs;
       a.C_bs = view->C_bs;
     }
-    (void)prepare_ws(c, B, a);   // allocated above: only sets the pointers
     return a;
   };
+  int rc;
   if (init) {
     if (B > c->scratch_n) {
       if (c->scratch_i32) (void)hipFree(c->scratch_i32);
@@ -310,16 +371,16 @@ int mpcontrol_impl(hmpc_ctx* c, int64_t B, int init, const double* x_in, const d
     int32_t* s1 = c->scratch_i32;
     int32_t* i1 = c->scratch_i32 + B;
     // pass 1: linearise about [x_in; x_ref]  (src/mpc_cvx_euler_3f.py:50-58)
-    if (!hmpc::launch_solve(c->variant, c->N, args(s1, i1, nullptr, 1), s)) return HMPC_ERR_UNSUPPORTED;
-    // pass 2: linearise about x* of pass 1 (in place: each workgroup stages
-    // its x_lin in LDS before writing x*)
-    hmpc::launch_solve(c->variant, c->N, args(status, iters, obj, 0), s);
+    if ((rc = run_solve(c, args(s1, i1, nullptr, 1), s)) != HMPC_OK) return rc;
+    // pass 2: linearise about x* of pass 1 (in place: each workgroup reads
+    // its x_lin before writing x*)
+    if ((rc = run_solve(c, args(status, iters, obj, 0), s)) != HMPC_OK) return rc;
     const int tpb = 256;
     hipLaunchKernelGGL(combine_status, dim3((unsigned)((B + tpb - 1) / tpb)), dim3(tpb), 0, s, B,
                        s1, i1, status, iters);
   } else {
     // time shift of the previous x*  (src/mpc_cvx_euler_3f.py:59-62)
-    if (!hmpc::launch_solve(c->variant, c->N, args(status, iters, obj, 2), s)) return HMPC_ERR_UNSUPPORTED;
+    if ((rc = run_solve(c, args(status, iters, obj, 2), s)) != HMPC_OK) return rc;
   }
   HMPC_HIP(c, hipGetLastError());
   return HMPC_OK;

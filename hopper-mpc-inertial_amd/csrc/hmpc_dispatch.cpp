@@ -1,5 +1,9 @@
-// Maps (variant, N) onto the per-horizon launchers compiled from
-// hmpc_kernels.hip (one object per horizon, see build.sh).
+// Maps (variant, N, precision) onto a solve kernel:
+//   * a dedicated one-/two-wavefront kernel (hmpc_kernels.hip, one object per
+//     horizon in HMPC_HORIZON_LIST, see build.sh),
+//   * the Riccati kernel (hmpc_ric.hip) for every other N <= kRicNmax,
+//   * the generic dense kernel (hmpc_wide.hip) beyond that, and for the
+//     fp32 / fp64-generic A/B precisions.
 #include "hmpc_internal.h"
 
 #ifndef HMPC_HORIZON_LIST
@@ -12,16 +16,6 @@ namespace hmpc {
 HMPC_HORIZON_LIST(HMPC_DECL)
 #undef HMPC_DECL
 
-bool launch_solve(int variant, int N, const SolveArgs& a, hipStream_t s) {
-  if (variant != 2 && variant != 3) return false;
-  if (a.precision != 0) return launch_solve_wide(variant, N, a, s);
-#define HMPC_CASE(n) \
-  if (N == n) return launch_solve_n##n(variant, a, s);
-  HMPC_HORIZON_LIST(HMPC_CASE)
-#undef HMPC_CASE
-  return launch_solve_wide(variant, N, a, s);
-}
-
 bool horizon_compiled(int variant, int N) {
   if (variant != 2 && variant != 3) return false;
 #define HMPC_CASE(n) \
@@ -29,6 +23,40 @@ bool horizon_compiled(int variant, int N) {
   HMPC_HORIZON_LIST(HMPC_CASE)
 #undef HMPC_CASE
   return false;
+}
+
+Kernel pick_kernel(int variant, int N, int precision) {
+  if (variant != 2 && variant != 3 || N < 1) return Kernel::None;
+  switch (precision) {
+    case 1:
+    case 2:
+      return N <= kWideNmax ? Kernel::Wide : Kernel::None;
+    case 3:
+      return N <= kRicNmax ? Kernel::Riccati : Kernel::None;
+    case 0:
+      if (horizon_compiled(variant, N)) return Kernel::Dense;
+      if (N <= kRicNmax) return Kernel::Riccati;
+      return N <= kWideNmax ? Kernel::Wide : Kernel::None;
+    default:
+      return Kernel::None;
+  }
+}
+
+bool launch_solve(int variant, int N, const SolveArgs& a, hipStream_t s) {
+  switch (pick_kernel(variant, N, a.precision)) {
+    case Kernel::Dense:
+#define HMPC_CASE(n) \
+  if (N == n) return launch_solve_n##n(variant, a, s);
+      HMPC_HORIZON_LIST(HMPC_CASE)
+#undef HMPC_CASE
+      return false;
+    case Kernel::Riccati:
+      return launch_solve_ric(variant, N, a, s);
+    case Kernel::Wide:
+      return launch_solve_wide(variant, N, a, s);
+    default:
+      return false;
+  }
 }
 
 bool horizon_supported(int variant, int N) {

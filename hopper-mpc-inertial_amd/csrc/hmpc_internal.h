@@ -40,9 +40,35 @@ struct SolveArgs {
   int64_t ws_stride;   // in elements of the arithmetic type
   int ws_groups;
   // 0: fp64 (dedicated kernel when the horizon has one), 1: fp32 generic
-  // kernel, 2: fp64 generic kernel (HMPC_PREC_*)
+  // kernel, 2: fp64 generic kernel, 3: fp64 Riccati kernel (HMPC_PREC_*)
   int precision;
+  // Active-set overflow (hmpc_ric.hip): an instance whose active set outgrows
+  // the LDS capacity of its kernel appends its index to ovf_list (count in
+  // *ovf_count, zeroed before the launch) and is re-solved by the overflow
+  // pass with capacity 6N (R in the global workspace rws, rws_stride doubles
+  // per resident workgroup).  ovf_count == nullptr: overflow = ST_NUMERICAL.
+  int32_t* ovf_count;
+  int32_t* ovf_list;
+  double* rws;
+  int64_t rws_stride;
 };
+
+// The Riccati kernel (hmpc_ric.hip): any horizon 1 <= N <= kRicNmax, one
+// wavefront per instance.
+constexpr int kRicNmax = 64;
+constexpr int ST_OVERFLOW = 4;   // internal: re-solved by the overflow pass
+// LDS capacity of R for the main pass at horizon N
+inline int ric_qcap(int N) {
+  const int nv = 6 * N;
+  const int cap = N <= 32 ? 40 : 64;
+  return nv < cap ? nv : cap;
+}
+// dynamic LDS bytes of the Riccati kernel at horizon N (R in LDS with
+// capacity qcap, or none when qcap == 0: overflow pass)
+size_t ric_lds_bytes(int N, int qcap);
+bool launch_solve_ric(int variant, int N, const SolveArgs& a, hipStream_t stream);
+// the overflow pass over a.ovf_list (count on the device), <= groups workgroups
+bool launch_solve_ric_overflow(int variant, int N, const SolveArgs& a, int groups, hipStream_t s);
 
 // Horizons without a dedicated kernel run on the generic kernel up to this N.
 constexpr int kWideNmax = 128;
@@ -106,8 +132,12 @@ struct PlantArgs {
 void launch_plant(const PlantArgs& a, hipStream_t s);
 void launch_convert(int64_t B, const double* X, double* x, hipStream_t s);
 
-// Launch the solve kernel for (variant, N).  Returns false when no kernel
-// is compiled for that combination.
+// Which kernel solves (variant, N) at a precision (HMPC_PREC_*).
+enum class Kernel { None, Dense, Riccati, Wide };
+Kernel pick_kernel(int variant, int N, int precision);
+// Launch the solve kernel for (variant, N, a.precision).  Returns false when
+// no kernel serves that combination.  Dense and Riccati kernels honour
+// a.ovf_count (the caller then runs launch_solve_ric_overflow).
 bool launch_solve(int variant, int N, const SolveArgs& a, hipStream_t stream);
 // the generic-horizon kernel (any 1 <= N <= kWideNmax); a.ws must be set
 bool launch_solve_wide(int variant, int N, const SolveArgs& a, hipStream_t stream);

@@ -1240,7 +1240,9 @@ solve_kernel(SolveArgs a) {
       HMPC_TIC(t_upd);
       if (has_z && t == t2) {
         // ---- add p: new basis column w_perp / |w_perp|, R column [c; rho] ----
-        if (qu >= QMAX) { status = ST_NUMERICAL; done = true; break; }
+        // active set beyond the register/LDS capacity: handed to the
+        // overflow pass (hmpc_ric.hip, capacity NV) when the caller set one up
+        if (qu >= QMAX) { status = a.ovf_count ? ST_OVERFLOW : ST_NUMERICAL; done = true; break; }
         const double rho = sqrt(zn);
         const double qn = wp / rho;
         // (selects over every register, not a branch per index: branches that
@@ -1314,6 +1316,16 @@ solve_kernel(SolveArgs a) {
     }
   }
   HMPC_STAMP(7);
+
+  // an overflowed instance writes nothing but its status and its place in
+  // the overflow list (x_lin may be this solve's input, mpcontrol shift)
+  if (uni(status) == ST_OVERFLOW) {
+    if (tid == 0) {
+      a.status[b] = ST_OVERFLOW;
+      a.ovf_list[atomicAdd(a.ovf_count, 1)] = (int32_t)b;
+    }
+    return;
+  }
 
   // ---------------- phase 7: outputs ----------------------------------------
   // u* straight out; x* by a lane-parallel forward simulation (lane r < 12

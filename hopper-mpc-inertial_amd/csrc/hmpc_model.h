@@ -213,11 +213,11 @@ __device__ __forceinline__ R bd_dot(int c2, const R (&y)[12], const R* bw, R dtm
 // Mpc.gen_dt_dynamics for stage k (3f :71-94, 2f :70-94): cos/sin of the
 // linearisation yaw and rows 9..11 of Bd_k (rows 6..8 are bv(); the rest of
 // Bd_k is zero).  xlin: [N][12] linearisation rows, pf: [N][3].
+// Same from values: psi = x_lin[k][5], p = x_lin[k][0:3], pfk = pf[k].
 template <int VAR, typename R>
-__device__ __forceinline__ void stage_dynamics(int k, const R* xlin, const R* pf,
-                                               const double (&Jinv)[9], const double (&rh)[3], R dt,
-                                               R* cs, R* bwo) {
-  const R psi = xlin[12 * k + 5];
+__device__ __forceinline__ void stage_dynamics_vals(int k, R psi, const R (&p)[3], const R (&pfk)[3],
+                                                    const double (&Jinv)[9], const double (&rh)[3],
+                                                    R dt, R* cs, R* bwo) {
   R sp, cp;
   if constexpr (sizeof(R) == 4) sincosf(psi, &sp, &cp);
   else sincos(psi, &sp, &cp);
@@ -225,7 +225,7 @@ __device__ __forceinline__ void stage_dynamics(int k, const R* xlin, const R* pf
   const R Rz[3][3] = {{cp, sp, R(0)}, {-sp, cp, R(0)}, {R(0), R(0), R(1)}};
   R d[3], rf[3];
 #pragma unroll
-  for (int i = 0; i < 3; ++i) d[i] = pf[3 * k + i] - xlin[12 * k + i];
+  for (int i = 0; i < 3; ++i) d[i] = pfk[i] - p[i];
   // rf = rh + Rz (pf - p)   (:84)
 #pragma unroll
   for (int i = 0; i < 3; ++i) rf[i] = R(rh[i]) + (Rz[i][0] * d[0] + Rz[i][1] * d[1] + Rz[i][2] * d[2]);
@@ -279,6 +279,15 @@ __device__ __forceinline__ void stage_dynamics(int k, const R* xlin, const R* pf
     }
   cs[2 * k] = cp;
   cs[2 * k + 1] = sp;
+}
+
+template <int VAR, typename R>
+__device__ __forceinline__ void stage_dynamics(int k, const R* xlin, const R* pf,
+                                               const double (&Jinv)[9], const double (&rh)[3], R dt,
+                                               R* cs, R* bwo) {
+  const R p[3] = {xlin[12 * k], xlin[12 * k + 1], xlin[12 * k + 2]};
+  const R pfk[3] = {pf[3 * k], pf[3 * k + 1], pf[3 * k + 2]};
+  stage_dynamics_vals<VAR, R>(k, xlin[12 * k + 5], p, pfk, Jinv, rh, dt, cs, bwo);
 }
 
 }  // namespace hmpc

@@ -70,6 +70,8 @@ extern "C" {
 #define HMPC_PREC_F32 1           /* fp32 arithmetic (generic kernel; BASELINE configs[4]:
                                      the tolerance/throughput trade-off)          */
 #define HMPC_PREC_F64_GENERIC 2   /* fp64 on the generic kernel (its fp32 twin's A/B) */
+#define HMPC_PREC_F64_RICCATI 3   /* fp64 on the Riccati kernel (any N <= 64; the default
+                                     for horizons without a dedicated kernel)     */
 
 typedef struct hmpc_ctx hmpc_ctx;
 
@@ -78,9 +80,13 @@ int hmpc_version(void);
 
 /* Which horizons have a dedicated (one- or two-wavefront) kernel for
    `variant`; writes up to `cap` values into `Ns`, returns the count.  Every
-   other horizon 1 <= N <= 128 (e.g. the Runner's N = 60) is solved by the
-   generic-horizon kernel out of a per-context device workspace; calls on one
-   context are then expected to be stream-ordered. */
+   other horizon 1 <= N <= 64 (e.g. the Runner's N = 60) is solved by the
+   Riccati kernel (one wavefront per instance, the condensed Hessian factored
+   by a backward Riccati recursion), 64 < N <= 128 by the generic dense kernel.
+   Every solve with N <= 64 re-solves the rare instances whose active set
+   outgrows its kernel's capacity in an overflow pass (capacity 6N).  The
+   context's workspaces are shared by its calls: calls on one context are
+   expected to be stream-ordered. */
 int hmpc_supported_horizons(int variant, int* Ns, int cap);
 
 /* Mpc.__init__: t = MPC sampling time (s), N = horizon, m (kg), g (m/s^2),
