@@ -38,6 +38,9 @@ struct hmpc_ctx {
   int32_t* ovf = nullptr;
   int64_t ovf_cap = 0;
   double* rws = nullptr;
+  // Riccati kernel: per-workgroup K / G^-1 workspace of its resident grid
+  double* kws = nullptr;
+  int ric_groups = 0;
   hipStream_t own_stream = nullptr;
 };
 
@@ -72,6 +75,8 @@ hmpc::SolveArgs make_args(hmpc_ctx* c, int64_t B, const double* x_in, const doub
   a.pf_bs = 3 * (int64_t)N; a.pf_rs = 3;
   a.C_bs = N;
   a.ws = nullptr; a.ws_stride = 0; a.ws_groups = 0;
+  a.ovf_count = nullptr; a.ovf_list = nullptr; a.rws = nullptr; a.rws_stride = 0;
+  a.work = nullptr; a.kws = nullptr; a.kws_stride = 0; a.ric_groups = 0;
   a.precision = c->precision;
   return a;
 }
@@ -106,19 +111,22 @@ int prepare_ws(hmpc_ctx* c, int64_t B, hmpc::SolveArgs& a) {
   return HMPC_OK;
 }
 
-// Overflow pass geometry: workgroups (each with an R block of capacity 6N in
-// global memory) looping over the instances whose active set outgrew the
-// main kernel's capacity.
+// Overflow pass geometry: workgroups (each with an R block of capacity 6N and
+// a K / G^-1 workspace in global memory) looping over the instances whose
+// active set outgrew the main kernel's capacity.
 constexpr int kOvfGroups = 128;
 
-int prepare_ovf(hmpc_ctx* c, int64_t B, hmpc::SolveArgs& a) {
+// Buffers of the dense / Riccati kernels: [overflow count | instance counter |
+// pad | overflow list], the overflow pass's blocks, the Riccati kernel's
+// per-workgroup K / G^-1 workspace.
+int prepare_ric(hmpc_ctx* c, int64_t B, hmpc::SolveArgs& a) {
   const hmpc::Kernel k = hmpc::pick_kernel(c->variant, c->N, c->precision);
   a.ovf_count = nullptr; a.ovf_list = nullptr; a.rws = nullptr; a.rws_stride = 0;
+  a.work = nullptr; a.kws = nullptr; a.kws_stride = 0; a.ric_groups = 0;
   if ((k != hmpc::Kernel::Dense && k != hmpc::Kernel::Riccati) || c->N > hmpc::kRicNmax) return HMPC_OK;
-  const int64_t nv = 6 * (int64_t)c->N;
-  const int64_t stride = ((nv * (nv + 1) / 2) + 15) & ~(int64_t)15;
+  const int64_t rstride = hmpc::ric_rws_stride(c->N);
   if (!c->rws) {
-    hipError_t e = hipMalloc(&c->rws, sizeof(double) * stride * kOvfGroups);
+    hipError_t e = hipMalloc(&c->rws, sizeof(double) * rstride * kOvfGroups);
     if (e != hipSuccess) { c->rws = nullptr; c->err = "overflow workspace hipMalloc"; return HMPC_ERR_NOMEM; }
   }
   if (B > c->ovf_cap) {
@@ -130,9 +138,22 @@ int prepare_ovf(hmpc_ctx* c, int64_t B, hmpc::SolveArgs& a) {
     c->ovf_cap = B;
   }
   a.ovf_count = c->ovf;
+  a.work = c->ovf + 1;
   a.ovf_list = c->ovf + 4;
   a.rws = c->rws;
-  a.rws_stride = stride;
+  a.rws_stride = rstride;
+  if (k == hmpc::Kernel::Riccati) {
+    if (c->ric_groups == 0) {
+      const int g = hmpc::ric_groups(c->variant, c->N);
+      if (g < 1) { c->err = "Riccati kernel occupancy query"; return HMPC_ERR_HIP; }
+      hipError_t e = hipMalloc(&c->kws, sizeof(double) * hmpc::ric_kws_stride(c->N) * g);
+      if (e != hipSuccess) { c->kws = nullptr; c->err = "Riccati workspace hipMalloc"; return HMPC_ERR_NOMEM; }
+      c->ric_groups = g;
+    }
+    a.kws = c->kws;
+    a.kws_stride = hmpc::ric_kws_stride(c->N);
+    a.ric_groups = c->ric_groups;
+  }
   return HMPC_OK;
 }
 
@@ -141,10 +162,10 @@ int prepare_ovf(hmpc_ctx* c, int64_t B, hmpc::SolveArgs& a) {
 int run_solve(hmpc_ctx* c, hmpc::SolveArgs a, hipStream_t s) {
   int rc = prepare_ws(c, a.B, a);
   if (rc != HMPC_OK) return rc;
-  rc = prepare_ovf(c, a.B, a);
+  rc = prepare_ric(c, a.B, a);
   if (rc != HMPC_OK) return rc;
-  if (a.ovf_count) {
-    hipError_t e = hipMemsetAsync(a.ovf_count, 0, sizeof(int32_t), s);
+  if (a.ovf_count) {   // overflow count and instance counter
+    hipError_t e = hipMemsetAsync(a.ovf_count, 0, 2 * sizeof(int32_t), s);
     if (e != hipSuccess) return fail_hip(c, e, "hipMemsetAsync(overflow count)");
   }
   if (!hmpc::launch_solve(c->variant, c->N, a, s)) {
@@ -221,6 +242,7 @@ int hmpc_destroy(hmpc_ctx* c) {
   if (c->wsbuf) (void)hipFree(c->wsbuf);
   if (c->ovf) (void)hipFree(c->ovf);
   if (c->rws) (void)hipFree(c->rws);
+  if (c->kws) (void)hipFree(c->kws);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   delete c;
   return HMPC_OK;
@@ -231,7 +253,7 @@ const char* hmpc_last_error(hmpc_ctx* c) { return c ? c->err.c_str() : ""; }
 int hmpc_set_precision(hmpc_ctx* c, int precision) {
   if (!c) return HMPC_ERR_ARG;
   if (precision != HMPC_PREC_F64 && precision != HMPC_PREC_F32 && precision != HMPC_PREC_F64_GENERIC &&
-      precision != HMPC_PREC_F64_RICCATI) {
+      precision != HMPC_PREC_F64_RICCATI && precision != HMPC_PREC_F64_DENSE) {
     c->err = "unknown precision";
     return HMPC_ERR_ARG;
   }

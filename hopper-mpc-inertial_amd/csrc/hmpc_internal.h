@@ -51,11 +51,19 @@ struct SolveArgs {
   int32_t* ovf_list;
   double* rws;
   int64_t rws_stride;
+  // Riccati kernel (persistent): instance counter (zeroed before the launch),
+  // resident workgroups and their K / G^-1 workspace (kws_stride doubles each)
+  int32_t* work;
+  int ric_groups;
+  double* kws;
+  int64_t kws_stride;
 };
 
 // The Riccati kernel (hmpc_ric.hip): any horizon 1 <= N <= kRicNmax, one
 // wavefront per instance.
 constexpr int kRicNmax = 64;
+// default precision: dedicated dense kernels win up to this horizon
+constexpr int kDenseNmax = 10;
 constexpr int ST_OVERFLOW = 4;   // internal: re-solved by the overflow pass
 // LDS capacity of R for the main pass at horizon N
 inline int ric_qcap(int N) {
@@ -66,6 +74,9 @@ inline int ric_qcap(int N) {
 // dynamic LDS bytes of the Riccati kernel at horizon N (R in LDS with
 // capacity qcap, or none when qcap == 0: overflow pass)
 size_t ric_lds_bytes(int N, int qcap);
+int64_t ric_kws_stride(int N);   // per-workgroup K / G^-1 workspace (doubles)
+int64_t ric_rws_stride(int N);   // per-workgroup overflow block: R (6N capacity) + workspace
+int ric_groups(int variant, int N);   // resident workgroups of the main Riccati kernel
 bool launch_solve_ric(int variant, int N, const SolveArgs& a, hipStream_t stream);
 // the overflow pass over a.ovf_list (count on the device), <= groups workgroups
 bool launch_solve_ric_overflow(int variant, int N, const SolveArgs& a, int groups, hipStream_t s);

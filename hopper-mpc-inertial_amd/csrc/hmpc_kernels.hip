@@ -94,15 +94,6 @@ __device__ __forceinline__ int opaque_zero() {
   return z;
 }
 
-// 1/sqrt(p) to ~1 ulp without the IEEE sqrt + divide sequences (two dependent
-// chains of ~15 f64 ops each): hardware v_rsq_f64 estimate, then one
-// third-order correction y (1 + e/2 + 3e^2/8), e = 1 - p y^2.
-__device__ __forceinline__ double rsq_nr(double p) {
-  const double y = __builtin_amdgcn_rsq(p);
-  const double e = fma(-(p * y), y, 1.0);
-  return fma(y * e, fma(0.375, e, 0.5), y);
-}
-
 // LDS loads the scheduler cannot move.  hipcc sinks prefetches next to their
 // use and then waits with lgkmcnt(0); these are issued where they stand, and
 // the value is valid only after the matching lds_wait (s_waitcnt lgkmcnt(n),

@@ -34,6 +34,16 @@ __device__ __forceinline__ float rdlane(float x, int l) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), l));
 }
 __device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
+
+// 1/sqrt(p) to ~1 ulp without the IEEE sqrt + divide sequences (two dependent
+// chains of ~15 f64 ops each): hardware v_rsq_f64 estimate, then one
+// third-order correction y (1 + e/2 + 3e^2/8), e = 1 - p y^2.
+__device__ __forceinline__ double rsq_nr(double p) {
+  const double y = __builtin_amdgcn_rsq(p);
+  const double e = fma(-(p * y), y, 1.0);
+  return fma(y * e, fma(0.375, e, 0.5), y);
+}
+
 // x of lane (r + D) within r's row of 16 lanes (D < 0: lane r - |D|); a DPP
 // row shift -- a VALU modifier, no LDS round trip like a bpermute.  Lanes
 // whose source falls outside their row read 0.

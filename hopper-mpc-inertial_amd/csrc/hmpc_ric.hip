@@ -46,7 +46,7 @@ constexpr int RT = 64;   // one wavefront per workgroup
 // LDS layout (in doubles) for a runtime horizon N and active-set capacity cap
 // (R in LDS only when r_lds).
 struct RicLay {
-  int XIN, CC, CS, BW, ZB, ZN, ZD, MISC, VV, SV, ZV, NB, MU, KM, GI, UA, ACT, CB, GV, SD, RM, U0, total;
+  int XIN, CC, CS, BW, ZB, ZN, ZD, MISC, VV, SV, ZV, NB, MU, UA, ACT, CB, GV, SD, RM, U0, total;
   __host__ __device__ RicLay(int N, int cap, bool r_lds) {
     const int NV = 6 * N;
     auto up2 = [](int x) { return (x + 1) & ~1; };   // 16-B alignment of every array
@@ -64,35 +64,63 @@ struct RicLay {
     ZV = o; o += NV;              // z = H^-1 (n_p - N_A r)
     NB = o; o += NV;              // right-hand side of H^-1 (n_p, n_p - N_A r)
     MU = o; o += NV;              // sweep scratch (mu, then G^-1 mu)
-    KM = o; o += 72 * N;          // K_k [6][12]
-    GI = o; o = up2(o + 21 * N);  // G_k^-1, packed lower triangle
     UA = o; o = up2(o + cap);     // active multipliers
     ACT = o; o = up2(o + cap);    // active ids (int)
     CB = o; o = up2(o + cap);     // scratch
     GV = o; o += 2 * up2(cap);    // Givens of a drop
     SD = o; o = up2(o + cap);     // subdiagonal scratch
-    U0 = o;                       // union: x_ref (12N) | Riccati scratch (468)
-    o += (12 * N > 468 ? 12 * N : 468);
+    U0 = o;                       // union: x_ref (12N) | Riccati scratch (568)
+    o += (12 * N > 568 ? 12 * N : 568);
     RM = o; if (r_lds) o = up2(o + cap * (cap + 1) / 2);   // packed upper R
     total = o;
   }
 };
 
-// Riccati scratch inside the union
-constexpr int PS_OFF = 0, M1_OFF = 144, TS_OFF = 288, FS_OFF = 360, GS_OFF = 432;
+// Riccati scratch inside the union (P, P A, P B, B'P A, G, Dinv, K_k)
+constexpr int PS_OFF = 0, M1_OFF = 144, TS_OFF = 288, FS_OFF = 360, GS_OFF = 432, DL_OFF = 468,
+              KL_OFF = 490;
+
+// Global workspace of one workgroup (doubles): K_k [6][12] and G_k^-1 (packed
+// lower) of every stage -- written by the factorisation, read by every sweep
+// (L2-resident: a few workgroups per CU)
+__host__ __device__ inline int64_t ric_kws_doubles(int N) { return ((93 * (int64_t)N) + 15) & ~(int64_t)15; }
 
 __device__ __forceinline__ int loff(int r) { return (r * (r + 1)) >> 1; }
 
-__device__ __forceinline__ void wsync() { __syncthreads(); }
+// Ordering point between lanes of the one wavefront of a workgroup: LDS
+// instructions of a wave execute in order, so only the compiler must be kept
+// from reordering them.  Global-memory hand-offs between lanes (the K / G^-1
+// workspace, the overflow pass's R) use gsync() = a workgroup barrier.
+__device__ __forceinline__ void wsync() { __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront"); }
+__device__ __forceinline__ void gsync() { __syncthreads(); }
 
-// inclusive prefix sum over the wave (lane order)
+// Diagnostic build only (-DHMPC_STAMPS, tools/ric_stamps.py): s_memtime
+// cycles per phase, accumulated, written over the instance's x* row.
+#ifdef HMPC_STAMPS
+#define RS_T(v) const long long v = __builtin_amdgcn_s_memtime()
+#define RS_ACC(slot, v) (rst_[slot] += __builtin_amdgcn_s_memtime() - (v))
+#else
+#define RS_T(v) ((void)0)
+#define RS_ACC(slot, v) ((void)0)
+#endif
+
+// inclusive prefix sum over the wave (lane order): Hillis-Steele inside each
+// row of 16 lanes by DPP row shifts, then the row broadcasts of lanes 15 and
+// 31 into the rows above (VALU modifiers, no LDS round trip)
+template <int CTRL, int RM>
+__device__ __forceinline__ double dpp0(double x) {   // 0 where the source is out of range / masked
+  const long long b = __double_as_longlong(x);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffffLL), CTRL, RM, 0xf, true);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, RM, 0xf, true);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
 __device__ __forceinline__ double wave_scan(double x) {
-  const int lane = threadIdx.x;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const double y = __shfl_up(x, d);
-    if (lane >= d) x += y;
-  }
+  x += dpp0<0x111, 0xf>(x);   // row_shr:1
+  x += dpp0<0x112, 0xf>(x);   // row_shr:2
+  x += dpp0<0x114, 0xf>(x);   // row_shr:4
+  x += dpp0<0x118, 0xf>(x);   // row_shr:8
+  x += dpp0<0x142, 0xa>(x);   // row_bcast:15 into rows 1, 3
+  x += dpp0<0x143, 0xc>(x);   // row_bcast:31 into rows 2, 3
   return x;
 }
 
@@ -114,7 +142,7 @@ __device__ __forceinline__ void vset(double (&v)[ENT], int i, double x) {
 
 template <int VAR, int ENT>
 __device__ void ric_solve(const SolveArgs& a, const int N, const int64_t b, double* sm, double* Rm,
-                          const int cap) {
+                          const int cap, double* kw) {
   const RicLay L(N, cap, false);
   const int lane = threadIdx.x;
   const int NV = 6 * N;
@@ -132,14 +160,19 @@ __device__ void ric_solve(const SolveArgs& a, const int N, const int64_t b, doub
   double* zv = sm + L.ZV;
   double* nb = sm + L.NB;
   double* mu_ = sm + L.MU;
-  double* km = sm + L.KM;
-  double* gi = sm + L.GI;
+  double* km = kw;            // K_k (global workspace)
+  double* gi = kw + 72 * N;   // G_k^-1 (global workspace)
   double* ua = sm + L.UA;
   int* act = reinterpret_cast<int*>(sm + L.ACT);
   double* gv = sm + L.GV;
   double* sdg = sm + L.SD;
   double* un = sm + L.U0;
 
+#ifdef HMPC_STAMPS
+  long long rst_[16] = {0};
+#endif
+  RS_T(t_all);
+  RS_T(t_p0);
   // ---------------- phase 0: loads + gen_dt_dynamics (lane k < N) ----------
   // x_ref / pf / C may be strided views of a resident plan (path_plan_grab,
   // src/robotrunner.py:228-230); x_lin rows per shift_mode (3f :50-62)
@@ -164,6 +197,8 @@ __device__ void ric_solve(const SolveArgs& a, const int N, const int64_t b, doub
   }
   wsync();
 
+  RS_ACC(0, t_p0);
+  RS_T(t_p1);
   // ---------------- phase 1: free response, d_t, adjoint, gradient ----------
   // lane r < 12 holds component r.  d_t = kf Q (xbar_t - r_{t-1}) overwrites
   // x_ref row t-1; the gradient h = 2 Gamma' W (xbar - r) - 2 V ubar goes to
@@ -209,6 +244,8 @@ __device__ void ric_solve(const SolveArgs& a, const int N, const int64_t b, doub
   }
   wsync();
 
+  RS_ACC(1, t_p1);
+  RS_T(t_p2);
   // ---------------- phase 2: Riccati factorisation -------------------------
   int status = ST_SOLVED;
   {
@@ -234,15 +271,28 @@ __device__ void ric_solve(const SolveArgs& a, const int N, const int64_t b, doub
         if (r < 9) return c < 3 ? bv<VAR>(r - 6, c, dtm, cp, sp) : 0.0;
         return bwk[6 * (r - 9) + c];
       };
-      // (a) T = P B
-      for (int e = lane; e < 72; e += RT) {
-        const int i = e / 6, c = e - 6 * i;
-        double acc = 0.0;
+      RS_T(t_fa);
+      // (a) T = P B and M1 = P A (both read P only)
+      for (int e = lane; e < 216; e += RT) {
+        if (e < 72) {
+          const int i = e / 6, c = e - 6 * i;
+          double acc = 0.0;
 #pragma unroll
-        for (int r = 6; r < 12; ++r) acc = fma(P[12 * i + r], bent(r, c), acc);
-        T[e] = acc;
+          for (int r = 6; r < 12; ++r) acc = fma(P[12 * i + r], bent(r, c), acc);
+          T[e] = acc;
+        } else {
+          const int e2 = e - 72, i = e2 / 12, j = e2 - 12 * i;
+          double m1 = P[e2];
+          if (j >= 6 && j < 9) m1 = fma(dt, P[12 * i + j - 6], m1);
+          else if (j == 9) m1 += dt * (cp * P[12 * i + 3] - sp * P[12 * i + 4]);
+          else if (j == 10) m1 += dt * (sp * P[12 * i + 3] + cp * P[12 * i + 4]);
+          else if (j == 11) m1 = fma(dt, P[12 * i + 5], m1);
+          M1[e2] = m1;
+        }
       }
       wsync();
+      RS_ACC(11, t_fa);
+      RS_T(t_fb);
       // (b) G = 2V + B'T (identity rows for fixed variables), F = T'A
       for (int e = lane; e < 108; e += RT) {
         if (e < 36) {
@@ -264,9 +314,12 @@ __device__ void ric_solve(const SolveArgs& a, const int N, const int64_t b, doub
         }
       }
       wsync();
-      // (c) G = D D' (every lane, redundantly), Dinv; G^-1 = Dinv'Dinv packed
-      // (lanes e < 21); K = Dinv'(Dinv F) (lanes j < 12, one column each)
-      double D[21], Di[21];
+      RS_ACC(12, t_fb);
+      RS_T(t_fc);
+      // (c) G = D D' (every lane, redundantly) with reciprocal pivots (no
+      // fp64 divide or sqrt sequences), Dinv = D^-1; K = Dinv'(Dinv F) (lanes
+      // j < 12, one column each); Dinv to LDS for G^-1 = Dinv'Dinv (lanes < 21)
+      double D[21], Di[21], dinv[6];
 #pragma unroll
       for (int c = 0; c < 6; ++c) {
 #pragma unroll
@@ -276,32 +329,28 @@ __device__ void ric_solve(const SolveArgs& a, const int N, const int64_t b, doub
           for (int m = 0; m < d; ++m) s = fma(-D[loff(c) + m], D[loff(d) + m], s);
           if (d == c) {
             nbad += (s > 0.0) ? 0.0 : 1.0;
-            D[loff(c) + c] = sqrt(s > 0.0 ? s : 1.0);
+            dinv[c] = rsq_nr(s > 0.0 ? s : 1.0);
           } else {
-            D[loff(c) + d] = s / D[loff(d) + d];
+            D[loff(c) + d] = s * dinv[d];
           }
         }
       }
 #pragma unroll
       for (int c = 0; c < 6; ++c) {   // column c of Dinv: forward substitution of e_c
-        Di[loff(c) + c] = 1.0 / D[loff(c) + c];
+        Di[loff(c) + c] = dinv[c];
 #pragma unroll
         for (int r = c + 1; r < 6; ++r) {
           double s = 0.0;
 #pragma unroll
           for (int m = c; m < r; ++m) s = fma(D[loff(r) + m], Di[loff(m) + c], s);
-          Di[loff(r) + c] = -s / D[loff(r) + r];
+          Di[loff(r) + c] = -s * dinv[r];
         }
       }
+      double* Dl = un + DL_OFF;   // Dinv, packed lower
+      double* Kl = un + KL_OFF;   // K_k (the P update reads it)
+      if (lane == 0) {
 #pragma unroll
-      for (int c = 0; c < 6; ++c) {
-#pragma unroll
-        for (int d = 0; d <= c; ++d) {
-          double s = 0.0;
-#pragma unroll
-          for (int m = c; m < 6; ++m) s = fma(Di[loff(m) + c], Di[loff(m) + d], s);
-          if (lane == 0) gi[21 * k + loff(c) + d] = s;
-        }
+        for (int e = 0; e < 21; ++e) Dl[e] = Di[e];
       }
       if (lane < 12) {
         const int j = lane;
@@ -319,21 +368,23 @@ __device__ void ric_solve(const SolveArgs& a, const int N, const int64_t b, doub
 #pragma unroll
           for (int m = c; m < 6; ++m) s = fma(Di[loff(m) + c], y[m], s);
           km[72 * k + 12 * c + j] = s;
+          Kl[12 * c + j] = s;
         }
       }
       wsync();
-      if (k == 0) break;
-      // (d) P_k = 2Q + A'(P A) - F'K, lower triangle computed, mirrored
-      for (int e = lane; e < 144; e += RT) {
-        const int i = e / 12, j = e - 12 * i;
-        double m1 = P[e];
-        if (j >= 6 && j < 9) m1 = fma(dt, P[12 * i + j - 6], m1);
-        else if (j == 9) m1 += dt * (cp * P[12 * i + 3] - sp * P[12 * i + 4]);
-        else if (j == 10) m1 += dt * (sp * P[12 * i + 3] + cp * P[12 * i + 4]);
-        else if (j == 11) m1 = fma(dt, P[12 * i + 5], m1);
-        M1[e] = m1;
+      RS_ACC(13, t_fc);
+      RS_T(t_fd);
+      // (d) G^-1 = Dinv'Dinv (lanes < 21) and P_k = 2Q + A'(P A) - F'K (lower
+      // triangle, mirrored)
+      if (lane < 21) {   // G^-1 (c, d), c >= d: sum_{m >= c} Dinv[m][c] Dinv[m][d]
+        int c = 0;
+        while (loff(c + 1) <= lane) ++c;
+        const int d = lane - loff(c);
+        double s = 0.0;
+        for (int m = c; m < 6; ++m) s = fma(Dl[loff(m) + c], Dl[loff(m) + d], s);
+        gi[21 * k + lane] = s;
       }
-      wsync();
+      if (k == 0) break;
       for (int e = lane; e < 78; e += RT) {
         int i = 0;
         while (loff(i + 1) <= e) ++i;
@@ -344,53 +395,151 @@ __device__ void ric_solve(const SolveArgs& a, const int N, const int64_t b, doub
         else if (i == 10) pn += dt * (sp * M1[36 + j] + cp * M1[48 + j]);
         else if (i == 11) pn = fma(dt, M1[60 + j], pn);
 #pragma unroll
-        for (int c = 0; c < 6; ++c) pn = fma(-F[12 * c + i], km[72 * k + 12 * c + j], pn);
+        for (int c = 0; c < 6; ++c) pn = fma(-F[12 * c + i], Kl[12 * c + j], pn);
         if (i == j) pn += 2.0 * kQ[i];
         P[12 * i + j] = pn;
         P[12 * j + i] = pn;
       }
       wsync();
+      RS_ACC(14, t_fd);
     }
     if (nbad != 0.0) status = ST_NUMERICAL;
   }
+  gsync();   // K, G^-1 (global) visible to every lane of the workgroup
 
   // ---------------- H^-1 by two sweeps ----------------------------------------
-  // dst = H^-1 NB (NB kept; MU scratch)
+  // dst = H^-1 NB (NB kept; MU scratch).  Lanes 0..11 hold the 12 state
+  // (forward) / adjoint (backward) components; the cross-component terms of A
+  // come from DPP row shifts, the 6 inputs from lanes 0..5 by readlane.
+  //   backward: mu_j[c] = n_j[c] - B_j[:,c]'lam    (lane c < 6; lam[6..11] in SGPRs)
+  //             lam_j[i] = (A_j'lam)[i] + K_j[:,i]'mu_j   (lane i < 12)
+  //   per stage: w_j = G_j^-1 mu_j                (lane j)
+  //   forward:  u_k[r] = w_k[r] - K_k[r,:] x       (lane r < 6; x in SGPRs)
+  //             x_{k+1}[i] = (A_k x)[i] + B_k[i,:] u_k    (lane i < 12)
+  // Every step's data (K_k from the global workspace, B_k / w_k from LDS) is
+  // loaded two steps ahead (a three-deep register ring).
+  // per-lane constants of the A maps (see the shift comments below)
+  const double gA = (lane >= 6 && lane <= 8) || lane == 11 ? dt : 0.0;   // bwd s6, fixed
+  const double gB = (lane == 9 || lane == 10) ? dt : 0.0;                // bwd s6, * cos
+  const double gC = lane == 9 ? -dt : 0.0;                               // bwd s5, * sin
+  const double gD = lane == 10 ? dt : 0.0;                               // bwd s7, * sin
+  const double fA = lane < 3 || lane == 5 ? dt : 0.0;                    // fwd s6, fixed
+  const double fB = (lane == 3 || lane == 4) ? dt : 0.0;                 // fwd s6, * cos
+  const double fC = lane == 3 ? dt : 0.0;                                // fwd s7, * sin
+  const double fD = lane == 4 ? -dt : 0.0;                               // fwd s5, * sin
+  const int c6 = lane < 6 ? lane : 0;
+  // force map rows 6..8 of B_k = dtm (3f: I; 2f: Rz(psi)') as per-lane
+  // coefficients P + Q cos + S sin, branch-free:
+  //   k*[r] (backward, lane c < 6):  B[6+r][c]
+  //   r*[c] (forward, lane 6+r):     B[6+r][c]
+  double kP[3], kQ_[3], kS[3], rP[3], rQ[3], rS[3];
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+    const double on_b = lane == r ? dtm : 0.0, on_f = lane == 6 + r ? dtm : 0.0;
+    if constexpr (VAR == 3) {
+      kP[r] = on_b; kQ_[r] = 0.0; kS[r] = 0.0;
+      rP[r] = on_f; rQ[r] = 0.0; rS[r] = 0.0;
+    } else {   // Rz' = [[c, -s, 0], [s, c, 0], [0, 0, 1]]
+      kP[r] = r == 2 ? on_b : 0.0;
+      kQ_[r] = r < 2 ? on_b : 0.0;
+      kS[r] = r == 0 ? (lane == 1 ? -dtm : 0.0) : (r == 1 ? (lane == 0 ? dtm : 0.0) : 0.0);
+      rP[r] = r == 2 ? (lane == 8 ? dtm : 0.0) : 0.0;
+      rQ[r] = r < 2 ? on_f : 0.0;   // column r of row r: cos
+      rS[r] = r == 0 ? (lane == 7 ? dtm : 0.0) : (r == 1 ? (lane == 6 ? -dtm : 0.0) : 0.0);
+    }
+  }
+  const double m911 = (lane >= 9 && lane < 12) ? 1.0 : 0.0;
+  struct BwdL {
+    double cp, sp, st, b0, b1, b2, n, kc[6];
+  };
+  struct FwdL {
+    double cp, sp, w, kr[12], br[6];
+  };
+  auto load_b = [&](int j, BwdL& d) __attribute__((always_inline)) {
+    d.cp = cs[2 * j];
+    d.sp = cs[2 * j + 1];
+    d.st = cc[j];
+    d.b0 = bw[18 * j + c6];
+    d.b1 = bw[18 * j + 6 + c6];
+    d.b2 = bw[18 * j + 12 + c6];
+    d.n = nb[6 * j + c6];
+    const double* kcol = km + 72 * j + (lane < 12 ? lane : 0);
+#pragma unroll
+    for (int c = 0; c < 6; ++c) d.kc[c] = kcol[12 * c];
+    asm volatile("" ::: "memory");   // issue here, two steps ahead of the use
+  };
+  auto load_f = [&](int k, FwdL& d) __attribute__((always_inline)) {
+    d.cp = cs[2 * k];
+    d.sp = cs[2 * k + 1];
+    d.w = mu_[6 * k + c6];
+    const double* krow = km + 72 * k + 12 * c6;
+#pragma unroll
+    for (int c = 0; c < 12; ++c) d.kr[c] = krow[c];
+    const int rr = (lane >= 9 && lane < 12) ? lane - 9 : 0;
+#pragma unroll
+    for (int c = 0; c < 6; ++c) d.br[c] = bw[18 * k + 6 * rr + c];
+    asm volatile("" ::: "memory");   // issue here, two steps ahead of the use
+  };
   auto hinv = [&](double* dst) __attribute__((always_inline)) {
-    double lam = 0.0;
-    for (int j = N - 1; j >= 0; --j) {
-      const double cp = cs[2 * j], sp = cs[2 * j + 1];
-      const bool stance = cc[j] != 0.0;
-      const double l6 = rdlane(lam, 6), l7 = rdlane(lam, 7), l8 = rdlane(lam, 8);
-      const double l9 = rdlane(lam, 9), l10 = rdlane(lam, 10), l11 = rdlane(lam, 11);
-      double m = 0.0;
-      if (lane < 6) {
-        const int c = lane;
-        const double* bwj = bw + 18 * j;
-        double bc = bwj[c] * l9 + bwj[6 + c] * l10 + bwj[12 + c] * l11;
-        if (c < 3)
-          bc += bv<VAR>(0, c, dtm, cp, sp) * l6 + bv<VAR>(1, c, dtm, cp, sp) * l7 +
-                bv<VAR>(2, c, dtm, cp, sp) * l8;
-        const bool fr = c >= 3 || (stance && !(VAR == 2 && c == 1));
-        m = nb[6 * j + c] - (fr ? bc : 0.0);
-        mu_[6 * j + c] = m;
+    // ---- backward sweep
+    {
+      double li = 0.0;                                  // lam_{j+1}[lane]
+      double l6 = 0.0, l7 = 0.0, l8 = 0.0, l9 = 0.0, l10 = 0.0, l11 = 0.0;   // broadcast
+      auto bstep = [&](int j, const BwdL& d) __attribute__((always_inline)) {
+        double k6, k7, k8;
+        if constexpr (VAR == 3) {
+          k6 = kP[0]; k7 = kP[1]; k8 = kP[2];
+        } else {
+          k6 = fma(kQ_[0], d.cp, kS[0] * d.sp);
+          k7 = fma(kQ_[1], d.cp, kS[1] * d.sp);
+          k8 = kP[2];
+        }
+        const double bc = fma(k6, l6, fma(k7, l7, k8 * l8)) + fma(d.b0, l9, fma(d.b1, l10, d.b2 * l11));
+        const bool fr = lane >= 3 || (d.st != 0.0 && !(VAR == 2 && lane == 1));
+        const double m = fr ? d.n - bc : d.n;
+        if (lane < 6) mu_[6 * j + lane] = m;
+        if (j == 0) return;
+        const double m0 = rdlane(m, 0), m1 = rdlane(m, 1), m2 = rdlane(m, 2);
+        const double m3 = rdlane(m, 3), m4 = rdlane(m, 4), m5 = rdlane(m, 5);
+        // (A'lam)[i]: lanes 6..8 += dt lam[i-6]; 9 += dt (c lam3 - s lam4);
+        // 10 += dt (s lam3 + c lam4); 11 += dt lam5
+        const double s6 = row_shift<-6>(li), s5 = row_shift<-5>(li), s7 = row_shift<-7>(li);
+        double a0 = fma(fma(gB, d.cp, gA), s6, li), a1 = (gC * d.sp) * s5, a2 = (gD * d.sp) * s7;
+        a0 = fma(d.kc[0], m0, a0);
+        a1 = fma(d.kc[1], m1, a1);
+        a2 = fma(d.kc[2], m2, a2);
+        a0 = fma(d.kc[3], m3, a0);
+        a1 = fma(d.kc[4], m4, a1);
+        a2 = fma(d.kc[5], m5, a2);
+        li = lane < 12 ? (a0 + a1) + a2 : 0.0;
+        l6 = rdlane(li, 6); l7 = rdlane(li, 7); l8 = rdlane(li, 8);
+        l9 = rdlane(li, 9); l10 = rdlane(li, 10); l11 = rdlane(li, 11);
+      };
+      // (loads are unconditional -- out-of-range steps reload stage 0 -- so
+      // that the vmcnt/lgkmcnt waits stay counted, not drained)
+      BwdL R0, R1, R2;
+      load_b(N - 1, R0);
+      load_b(N >= 2 ? N - 2 : 0, R1);
+      for (int j = N - 1; j >= 0; j -= 3) {
+        load_b(j >= 2 ? j - 2 : 0, R2);
+        bstep(j, R0);
+        if (j < 1) break;
+        load_b(j >= 3 ? j - 3 : 0, R0);
+        bstep(j - 1, R1);
+        if (j < 2) break;
+        load_b(j >= 4 ? j - 4 : 0, R1);
+        bstep(j - 2, R2);
       }
-      if (j == 0) break;
-      const double m0 = rdlane(m, 0), m1 = rdlane(m, 1), m2 = rdlane(m, 2);
-      const double m3 = rdlane(m, 3), m4 = rdlane(m, 4), m5 = rdlane(m, 5);
-      double nl = adt_lane(lam, dt, cp, sp);
-      if (lane < 12) {
-        const double* kj = km + 72 * j + lane;
-        nl += ((kj[0] * m0 + kj[12] * m1) + (kj[24] * m2 + kj[36] * m3)) + (kj[48] * m4 + kj[60] * m5);
-      }
-      lam = lane < 12 ? nl : 0.0;
     }
     wsync();
+    // ---- w_j = G_j^-1 mu_j (lane-per-stage)
     for (int j = lane; j < N; j += RT) {
-      double mv[6], w[6];
+      double mv[6], w[6], g[21];
+      const double* gj = gi + 21 * j;
+#pragma unroll
+      for (int e = 0; e < 21; ++e) g[e] = gj[e];
 #pragma unroll
       for (int c = 0; c < 6; ++c) mv[c] = mu_[6 * j + c];
-      const double* g = gi + 21 * j;
 #pragma unroll
       for (int c = 0; c < 6; ++c) {
         double s = 0.0;
@@ -402,36 +551,61 @@ __device__ void ric_solve(const SolveArgs& a, const int N, const int64_t b, doub
       for (int c = 0; c < 6; ++c) mu_[6 * j + c] = w[c];
     }
     wsync();
-    double x = 0.0;
-    for (int k = 0; k < N; ++k) {
-      const double cp = cs[2 * k], sp = cs[2 * k + 1];
-      double xs[12];
+    // ---- forward sweep
+    {
+      double xi = 0.0;   // x_k[lane]
+      auto fstep = [&](int k, const FwdL& d) __attribute__((always_inline)) {
+        double xs[12];
 #pragma unroll
-      for (int i = 0; i < 12; ++i) xs[i] = rdlane(x, i);
-      double u = 0.0;
-      if (lane < 6) {
-        const double* kr = km + 72 * k + 12 * lane;
-        double a0 = mu_[6 * k + lane], a1 = 0.0;
+        for (int i = 0; i < 12; ++i) xs[i] = rdlane(xi, i);
+        double a0 = d.w, a1 = 0.0;
 #pragma unroll
         for (int c = 0; c < 12; c += 2) {
-          a0 = fma(-kr[c], xs[c], a0);
-          a1 = fma(-kr[c + 1], xs[c + 1], a1);
+          a0 = fma(-d.kr[c], xs[c], a0);
+          a1 = fma(-d.kr[c + 1], xs[c + 1], a1);
         }
-        u = a0 + a1;
-        dst[6 * k + lane] = u;
+        const double u = a0 + a1;
+        if (lane < 6) dst[6 * k + lane] = u;
+        const double u0 = rdlane(u, 0), u1 = rdlane(u, 1), u2 = rdlane(u, 2);
+        const double u3 = rdlane(u, 3), u4 = rdlane(u, 4), u5 = rdlane(u, 5);
+        // (A x)[i]: lanes 0..2 += dt x[i+6]; 3 += dt (c x9 + s x10);
+        // 4 += dt (c x10 - s x9); 5 += dt x11
+        const double s6 = row_shift<6>(xi), s5 = row_shift<5>(xi), s7 = row_shift<7>(xi);
+        // B rows: 6..8 the force map, 9..11 the stored rows of B_k
+        double r0, r1, r2;
+        if constexpr (VAR == 3) {
+          r0 = rP[0]; r1 = rP[1]; r2 = rP[2];
+        } else {
+          r0 = fma(rQ[0], d.cp, rS[0] * d.sp);
+          r1 = fma(rQ[1], d.cp, rS[1] * d.sp);
+          r2 = rP[2];
+        }
+        r0 = fma(m911, d.br[0], r0);
+        r1 = fma(m911, d.br[1], r1);
+        r2 = fma(m911, d.br[2], r2);
+        const double r3 = m911 * d.br[3], r4 = m911 * d.br[4], r5 = m911 * d.br[5];
+        double b0 = fma(fma(fB, d.cp, fA), s6, xi), b1 = (fC * d.sp) * s7, b2 = (fD * d.sp) * s5;
+        b0 = fma(r0, u0, b0);
+        b1 = fma(r1, u1, b1);
+        b2 = fma(r2, u2, b2);
+        b0 = fma(r3, u3, b0);
+        b1 = fma(r4, u4, b1);
+        b2 = fma(r5, u5, b2);
+        xi = lane < 12 ? (b0 + b1) + b2 : 0.0;
+      };
+      FwdL R0, R1, R2;
+      load_f(0, R0);
+      load_f(N >= 2 ? 1 : 0, R1);
+      for (int k = 0; k < N; k += 3) {
+        load_f(k + 2 < N ? k + 2 : N - 1, R2);
+        fstep(k, R0);
+        if (k + 1 >= N) break;
+        load_f(k + 3 < N ? k + 3 : N - 1, R0);
+        fstep(k + 1, R1);
+        if (k + 2 >= N) break;
+        load_f(k + 4 < N ? k + 4 : N - 1, R1);
+        fstep(k + 2, R2);
       }
-      const double u0 = rdlane(u, 0), u1 = rdlane(u, 1), u2 = rdlane(u, 2);
-      const double u3 = rdlane(u, 3), u4 = rdlane(u, 4), u5 = rdlane(u, 5);
-      double nx = ad_lane(x, dt, cp, sp);
-      if (lane >= 6 && lane < 9) {
-        const int r = lane - 6;
-        nx += bv<VAR>(r, 0, dtm, cp, sp) * u0 + bv<VAR>(r, 1, dtm, cp, sp) * u1 +
-              bv<VAR>(r, 2, dtm, cp, sp) * u2;
-      } else if (lane >= 9 && lane < 12) {
-        const double* bwr = bw + 18 * k + 6 * (lane - 9);
-        nx += ((bwr[0] * u0 + bwr[1] * u1) + (bwr[2] * u2 + bwr[3] * u3)) + (bwr[4] * u4 + bwr[5] * u5);
-      }
-      x = lane < 12 ? nx : 0.0;
     }
     wsync();
   };
@@ -444,14 +618,16 @@ __device__ void ric_solve(const SolveArgs& a, const int N, const int64_t b, doub
     }
     return wave_sum(s);
   };
-  // lane k: sum_{j <= k-2} zc (k-1-j) C_j X[fz_j] (the z-row of stage k over X)
+  // lane k: sum_{j <= k-2} zc (k-1-j) C_j X[fz_j] (the z-row of stage k over
+  // X) = zc * (exclusive scan of the exclusive scan of C_j X[fz_j])
   auto zdot = [&](const double* X) -> double {
-    const double aj = (lane < N && cc[lane] != 0.0) ? X[6 * lane + 2] : 0.0;
-    const double s1 = wave_scan(aj), s2 = wave_scan(aj * (double)lane);
-    const double t1 = __shfl_up(s1, 2), t2 = __shfl_up(s2, 2);
-    return lane >= 2 ? zc * ((double)(lane - 1) * t1 - t2) : 0.0;
+    const double aj = (lane < N && cc[lane < N ? lane : 0] != 0.0) ? X[6 * (lane < N ? lane : 0) + 2] : 0.0;
+    const double e1 = wave_scan(aj) - aj;
+    return zc * (wave_scan(e1) - e1);
   };
 
+  RS_ACC(2, t_p2);
+  RS_T(t_p3);
   // ---------------- phase 3: unconstrained optimum v0 = -H^-1 h --------------
   hinv(vv);
   // |n| of the z rows (lane k): zc sqrt(sum_{j <= k-2, stance} (k-1-j)^2)
@@ -465,7 +641,13 @@ __device__ void ric_solve(const SolveArgs& a, const int N, const int64_t b, doub
   }
   wsync();
 
+  RS_ACC(3, t_p3);
   // ---------------- phase 4: dual active set --------------------------------
+  // R lives in LDS (main pass) or global memory (overflow pass, ENT > 1)
+  auto rsync = [&]() __attribute__((always_inline)) {
+    if constexpr (ENT > 1) gsync();
+    else wsync();
+  };
   int iters = 0;
   if (xin[2] - kZmin < -kTol || zb[1] - kZmin < -kTol) status = ST_INFEAS;   // constant rows z_0, z_1
   const int max_iter = 4 * NV + 50;
@@ -513,6 +695,7 @@ __device__ void ric_solve(const SolveArgs& a, const int N, const int64_t b, doub
 
   bool done = status != ST_SOLVED;
   while (!done) {
+    RS_T(t_scan);
     // ---- slacks of my stage's constraints; the most violated ----
     const double vz = zdot(vv);
     double best = INFINITY;
@@ -549,7 +732,9 @@ __device__ void ric_solve(const SolveArgs& a, const int N, const int64_t b, doub
       }
     }
     wave_argmin(best, bid);
+    RS_ACC(4, t_scan);
     if (!(best < -kTol)) break;   // primal feasible: optimal
+    RS_T(t_s);
     const int p = uni(bid);
     const double bp = rhs_of(p);
     // n_p -> NB
@@ -559,16 +744,18 @@ __device__ void ric_solve(const SolveArgs& a, const int N, const int64_t b, doub
 #pragma unroll
       for (int c = 0; c < 6; ++c) nb[6 * j + c] = acc[c];
     }
-    wsync();
+    rsync();
     hinv(sv);                     // s = H^-1 n_p
     const double sn = vdot(nb, sv);
     const double szd = zdot(sv);
     if (lane < N) zd[lane] = szd;
-    wsync();
+    rsync();
+    RS_ACC(5, t_s);
     double uplus = 0.0;
     // ---- inner loop: step towards satisfying constraint p ----
     while (true) {
       if (++iters > max_iter) { status = ST_MAXIT; done = true; break; }
+      RS_T(t_c);
       // c = N_A' s, y = R^-T c, r = R^-1 y  (entry a in lane a % 64)
       double yv[ENT], rv[ENT];
 #pragma unroll
@@ -605,6 +792,8 @@ __device__ void ric_solve(const SolveArgs& a, const int N, const int64_t b, doub
         }
       }
       // z = H^-1 (n_p - N_A r), n_z' z
+      RS_ACC(6, t_c);
+      RS_T(t_z);
       const double* zsrc = sv;
       double zn = sn;
       if (q > 0) {
@@ -617,11 +806,13 @@ __device__ void ric_solve(const SolveArgs& a, const int N, const int64_t b, doub
         }
         // (the vget above is wave-uniform: every lane runs the same trip count
         // when N <= 64)
-        wsync();
+        rsync();
         hinv(zv);
         zsrc = zv;
         zn = vdot(nb, zv);
       }
+      RS_ACC(7, t_z);
+      RS_T(t_u);
       // partial step t1 (drop candidate) over r > 0
       double t1 = INFINITY;
       int kdrop = 0x7fffffff;
@@ -645,7 +836,7 @@ __device__ void ric_solve(const SolveArgs& a, const int N, const int64_t b, doub
         if (ai < q) ua[ai] = fma(-t, rv[e], ua[ai]);
       }
       uplus += t;
-      wsync();
+      rsync();
       if (has_z && t == t2) {
         // ---- add p: R column [y; sqrt(n_z'z)] ----
         if (q >= cap) {
@@ -665,7 +856,8 @@ __device__ void ric_solve(const SolveArgs& a, const int N, const int64_t b, doub
         }
         if (lane == (p >> 2) / 6) amask |= 1 << (4 * ((p >> 2) % 6) + (p & 3));
         ++q;
-        wsync();
+        rsync();
+        RS_ACC(8, t_u);
         break;
       }
       // ---- drop kdrop: delete its column of R, restore the triangle ----
@@ -677,10 +869,10 @@ __device__ void ric_solve(const SolveArgs& a, const int N, const int64_t b, doub
           for (int i0 = 0; i0 <= m + 1; i0 += RT) {
             const int i = i0 + lane;
             const double val = i <= m + 1 ? Rm[loff(m + 1) + i] : 0.0;
-            wsync();
+            rsync();
             if (i <= m) Rm[loff(m) + i] = val;
             if (i == m + 1) sdg[m] = val;
-            wsync();
+            rsync();
           }
         }
         for (int i0 = k; i0 + 1 < q; i0 += RT) {   // shift the active list
@@ -688,15 +880,15 @@ __device__ void ric_solve(const SolveArgs& a, const int N, const int64_t b, doub
           int an = 0;
           double un_ = 0.0;
           if (i + 1 < q) { an = act[i + 1]; un_ = ua[i + 1]; }
-          wsync();
+          rsync();
           if (i + 1 < q) { act[i] = an; ua[i] = un_; }
-          wsync();
+          rsync();
         }
         for (int l = k; l + 1 < q; ++l) {   // Givens on rows (l, l+1)
           const double aa = Rm[loff(l) + l], bb = sdg[l];
           const double hh = sqrt(aa * aa + bb * bb);
           const double cg = hh != 0.0 ? aa / hh : 1.0, sg = hh != 0.0 ? bb / hh : 0.0;
-          wsync();
+          rsync();
           if (lane == 0) Rm[loff(l) + l] = hh;
           for (int i0 = 0; i0 < q; i0 += RT) {
             const int mcol = i0 + lane;   // columns m > l hold rows l, l+1
@@ -706,14 +898,16 @@ __device__ void ric_solve(const SolveArgs& a, const int N, const int64_t b, doub
               Rm[loff(mcol) + l + 1] = -sg * rl + cg * rl1;
             }
           }
-          wsync();
+          rsync();
         }
         q = q - 1;
-        wsync();
+        rsync();
+        RS_ACC(8, t_u);
       }
     }
   }
 
+  RS_T(t_p5);
   // ---------------- phase 5: outputs ---------------------------------------
   // overflowed instances are re-solved by the overflow pass: write nothing
   // but the status (x_prev may be this solve's input)
@@ -770,8 +964,15 @@ __device__ void ric_solve(const SolveArgs& a, const int N, const int64_t b, doub
     }
     const double objv = wave_sum(objl);
     wsync();
+#ifdef HMPC_STAMPS
+    RS_ACC(9, t_p5);
+    RS_ACC(10, t_all);
+    if (a.x && lane == 0)
+      for (int i = 0; i < 16; ++i) reinterpret_cast<long long*>(a.x)[b * 12 * (N + 1) + i] = rst_[i];
+#else
     if (a.x)
       for (int i = lane; i < 12 * (N + 1); i += RT) a.x[b * 12 * (N + 1) + i] = xo[i];
+#endif
     if (lane == 0) {
       if (a.obj) a.obj[b] = objv;
       a.status[b] = status;
@@ -780,25 +981,37 @@ __device__ void ric_solve(const SolveArgs& a, const int N, const int64_t b, doub
   }
 }
 
+// Persistent: a.ric_groups workgroups, each with its slot of the K / G^-1
+// workspace, take instances off an atomic counter (a.work, zeroed with the
+// overflow count before the launch) until the batch is done.
 template <int VAR>
 __global__ void __launch_bounds__(RT) ric_kernel(SolveArgs a, int N, int cap) {
   extern __shared__ __attribute__((aligned(16))) double ric_sm[];
   const RicLay L(N, cap, true);
-  ric_solve<VAR, 1>(a, N, (int64_t)blockIdx.x, ric_sm, ric_sm + L.RM, cap);
+  double* kw = a.kws + (int64_t)blockIdx.x * a.kws_stride;
+  while (true) {
+    int b = 0;
+    if (threadIdx.x == 0) b = atomicAdd(a.work, 1);
+    b = __builtin_amdgcn_readfirstlane(b);
+    if (b >= a.B) break;
+    ric_solve<VAR, 1>(a, N, (int64_t)b, ric_sm, ric_sm + L.RM, cap, kw);
+    __syncthreads();
+  }
 }
 
-// the overflow pass: instances listed in a.ovf_list, capacity 6N, R in the
-// global workspace (one block of rws_stride doubles per workgroup)
+// the overflow pass: instances listed in a.ovf_list, capacity 6N, R and the
+// K / G^-1 workspace in the global block of the workgroup (rws_stride doubles)
 template <int VAR>
 __global__ void __launch_bounds__(RT) ric_overflow_kernel(SolveArgs a, int N) {
   extern __shared__ __attribute__((aligned(16))) double ric_sm[];
   const int n = *a.ovf_count;
   double* Rm = a.rws + (int64_t)blockIdx.x * a.rws_stride;
+  double* kw = Rm + (a.rws_stride - ric_kws_doubles(N));
   SolveArgs a2 = a;
   a2.ovf_count = nullptr;   // no further overflow: capacity is 6N
   for (int i = blockIdx.x; i < n; i += gridDim.x) {
     const int64_t b = a.ovf_list[i];
-    ric_solve<VAR, (6 * kRicNmax + 63) / 64>(a2, N, b, ric_sm, Rm, 6 * N);
+    ric_solve<VAR, (6 * kRicNmax + 63) / 64>(a2, N, b, ric_sm, Rm, 6 * N, kw);
     __syncthreads();
   }
 }
@@ -817,17 +1030,44 @@ size_t ric_lds_bytes(int N, int qcap) {
   return (size_t)L.total * sizeof(double);
 }
 
+int64_t ric_kws_stride(int N) { return ric_kws_doubles(N); }
+
+int64_t ric_rws_stride(int N) {
+  const int64_t nv = 6 * (int64_t)N;
+  return (((nv * (nv + 1) / 2) + 15) & ~(int64_t)15) + ric_kws_doubles(N);
+}
+
+int ric_groups(int variant, int N) {
+  const int cap = ric_qcap(N);
+  const size_t lds = ric_lds_bytes(N, cap);
+  int dev = 0, cus = 0, per = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+  hipError_t e;
+  if (variant == 3) {
+    if (!set_lds(ric_kernel<3>, lds)) return 0;
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, ric_kernel<3>, RT, lds);
+  } else {
+    if (!set_lds(ric_kernel<2>, lds)) return 0;
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, ric_kernel<2>, RT, lds);
+  }
+  if (e != hipSuccess || per < 1) per = 1;
+  return cus * per;
+}
+
 bool launch_solve_ric(int variant, int N, const SolveArgs& a, hipStream_t s) {
   if (N < 1 || N > kRicNmax || (variant != 2 && variant != 3)) return false;
   if (a.B <= 0) return true;
+  if (!a.work || !a.kws || a.ric_groups < 1) return false;
   const int cap = ric_qcap(N);
   const size_t lds = ric_lds_bytes(N, cap);
+  const unsigned g = (unsigned)(a.B < a.ric_groups ? a.B : a.ric_groups);
   if (variant == 3) {
     if (!set_lds(ric_kernel<3>, lds)) return false;
-    hipLaunchKernelGGL(ric_kernel<3>, dim3((unsigned)a.B), dim3(RT), lds, s, a, N, cap);
+    hipLaunchKernelGGL(ric_kernel<3>, dim3(g), dim3(RT), lds, s, a, N, cap);
   } else {
     if (!set_lds(ric_kernel<2>, lds)) return false;
-    hipLaunchKernelGGL(ric_kernel<2>, dim3((unsigned)a.B), dim3(RT), lds, s, a, N, cap);
+    hipLaunchKernelGGL(ric_kernel<2>, dim3(g), dim3(RT), lds, s, a, N, cap);
   }
   return true;
 }

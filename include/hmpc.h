@@ -71,7 +71,9 @@ extern "C" {
                                      the tolerance/throughput trade-off)          */
 #define HMPC_PREC_F64_GENERIC 2   /* fp64 on the generic kernel (its fp32 twin's A/B) */
 #define HMPC_PREC_F64_RICCATI 3   /* fp64 on the Riccati kernel (any N <= 64; the default
-                                     for horizons without a dedicated kernel)     */
+                                     for 10 < N <= 64)                            */
+#define HMPC_PREC_F64_DENSE 4     /* fp64 on the dedicated dense kernel of N (compiled
+                                     horizons only; the default for N <= 10)      */
 
 typedef struct hmpc_ctx hmpc_ctx;
 
