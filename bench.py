@@ -4,15 +4,18 @@
 One *step* = one pass of the hot path over one batch: every instance's
 ``Mpc.gen_dt_dynamics`` + ``Mpc.build_qp`` + ``Mpc.solve_qp``
 (src/mpc_cvx_euler_3f.py:71-160) on the GPU through the C ABI
-(``hmpc_solve_batch``), then -- for N > 1 ranks -- the RCCL all-gather of the
-per-instance objective and status, one packed collective per
-step on a side stream, overlapping the next step's solve
-(``hmpc_dist.ResultExchange``); the timed region ends after every exchange.
-Inputs are resident in HBM before the timed region starts.
+(``hmpc_solve_batch``: the solve kernel, then the active-set overflow pass),
+then -- for N > 1 ranks -- the RCCL all-gather of the per-instance objective
+and status, one packed collective per step on a side stream,
+overlapping the next step's solve (``hmpc_dist.ResultExchange``); the timed
+region ends after every exchange.  Inputs are resident in HBM before the
+timed region starts.
 
 Default workload = BASELINE.json configs[2]: 65536 randomised instances per
 GPU, 3f, horizon N = 10, --curve reference plan, fp64 (weak scaling: every
-rank solves its own 65536-instance shard of the global batch).
+rank solves its own 65536-instance shard).  ``--global-batch G`` instead
+splits a fixed global batch over the ranks (strong scaling; configs[3] is
+``--N 20 --straight --mu-sweep --global-batch 262144``).
 
 Launch:  python bench.py [--gpus 1] [--steps K] [--warmup W]
          python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
@@ -46,66 +49,135 @@ def algorithmic_bytes(N, with_mu=True):
     return 8 * (nin + nout) + 4
 
 
+def algorithmic_flops(kernel, N, iters, q):
+    """fp64 flops one solve needs in the algorithm the kernel runs (2 per
+    FMA; DESIGN.md 5 derives each term), as a closed form over the horizon N,
+    the active-set iterations and the active-set size q -- useful arithmetic,
+    not executed lanes.
+
+    dense (condensed, NV = 6N): Hessian rows 210 N(N+1) + Cholesky NV^3/3 +
+      unconstrained 2 NV^2 + per iteration (2 NV^2 + 4 q NV + q^2) + 400 N
+    Riccati: factorisation 4480 N + unconstrained 720 N + per iteration
+      (1440 N + 2 q^2 + 80 N) + 400 N
+    """
+    NV = 6 * N
+    if 'ric_kernel' in kernel:
+        return 4480 * N + 720 * N + iters * (1440 * N + 2 * q * q + 80 * N) + 400 * N
+    return 210 * N * (N + 1) + NV ** 3 / 3 + 2 * NV * NV + iters * (2 * NV * NV + 4 * q * NV + q * q) + 400 * N
+
+
+def workload_label(args, world):
+    """Which BASELINE.json config this run measures (configs[0] is the
+    reference's own CPU run.py, whose MPC horizon is N = 60)."""
+    gb = args.global_batch or args.batch * world
+    curve = not args.straight
+    if args.precision == 'f32' and args.variant == '3f' and args.N == 10:
+        return f'configs[4]: batch={gb}, 3f, N=10, fp32 (vs fp64) tolerance/throughput trade-off'
+    if args.variant == '2f' and args.N == 10 and not curve:
+        return f'configs[1]: batch={gb} randomised x0, 2f (planar, Fy=0), horizon N=10, fp64'
+    if args.variant == '3f' and args.N == 10 and curve:
+        return f'configs[2]: batch={gb} randomised x0 + --curve ref traj, 3f, horizon N=10, fp64'
+    if args.variant == '3f' and args.N == 20 and args.mu_sweep:
+        return (f'configs[3]: batch={gb}, 3f, horizon N=20 + friction-cone sweep, '
+                f'{"strong" if args.global_batch else "weak"} scaling over {world} GPU(s)')
+    if args.N == 60:
+        return (f'Runner horizon N=60 (configs[0]: run.py 3f --N_run=2000, src/robotrunner.py:46): '
+                f'batch={gb}, {args.variant}, {"--curve" if curve else "straight"}')
+    return (f'custom: batch={gb}, {args.variant}, N={args.N}, {"--curve" if curve else "straight"}'
+            f'{", mu sweep" if args.mu_sweep else ""}, {args.precision}')
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=20)
     ap.add_argument('--warmup', type=int, default=3)
-    ap.add_argument('--batch', type=int, default=65536, help='instances per GPU')
+    ap.add_argument('--batch', type=int, default=65536, help='instances per GPU (weak scaling)')
+    ap.add_argument('--global-batch', type=int, default=0,
+                    help='fixed global batch split over the ranks (strong scaling)')
     ap.add_argument('--variant', default='3f', choices=['3f', '2f'])
     ap.add_argument('--N', type=int, default=10)
     ap.add_argument('--straight', action='store_true', help='straight plan (default: --curve)')
     ap.add_argument('--mu-sweep', action='store_true', help='mu ~ U(0.3, 1.2)')
     ap.add_argument('--seed', type=int, default=2024)
-    ap.add_argument('--precision', default='f64', choices=['f64', 'f32', 'f64_generic'],
-                    help='configs[4]: f32 = fp32 arithmetic on the generic kernel; '
-                         'f64_generic = its fp64 twin (f64 = the dedicated fp64 kernel)')
-    ap.add_argument('--cpu-seconds', type=float, default=10.0,
-                    help='budget of the bounded CPU-baseline sample (0 disables)')
+    ap.add_argument('--precision', default='f64',
+                    choices=['f64', 'f32', 'f64_generic', 'f64_riccati', 'f64_dense'],
+                    help='f64 = the fastest fp64 kernel for N (default); f32 = fp32 one-wave '
+                         'kernel (configs[4]); others force a kernel for A/B runs')
+    ap.add_argument('--cpu-seconds', type=float, default=12.0,
+                    help='budget of the bounded CPU-baseline sample, split over its two legs '
+                         '(all cores, then one core); 0 disables')
     return ap.parse_args()
+
+
+def cpu_threads():
+    """The CPU share this process may use: its affinity set, capped by
+    OMP_NUM_THREADS (the GPU box sets 16 per GPU)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    omp = os.environ.get('OMP_NUM_THREADS')
+    if omp and omp.isdigit():
+        n = min(n, int(omp))
+    return max(1, n)
 
 
 def cpu_baseline(args, inst, gpu_u, gpu_status, budget_s):
     """Reported baseline, not the target: the oracle's C port (oracle/hmpc_port.c:
     the reference's gen_dt_dynamics/build_qp restated in C, condensed densely
     and solved exactly by a classic dual active set; OpenMP over instances)
-    timed on this host's cores over a bounded prefix of the same workload.
-    Also returns the parity of those instances against the GPU results."""
+    timed on this host over a bounded prefix of the same workload, on every
+    core of this process's CPU share and on one core.  Also returns the parity
+    of those instances against the GPU: max|du| where both solved, and every
+    (gpu status, port status) disagreement counted."""
     from oracle import port
     if budget_s <= 0:
         return None, None
-    try:
-        cores = len(os.sched_getaffinity(0))
-    except AttributeError:
-        cores = os.cpu_count() or 1
-    cores = max(1, min(cores, 16))   # the GPU box's CPU share per GPU
-    chunk = 256 * cores
     keys = ('x_in', 'x_lin', 'x_ref', 'pf', 'C')
-    port.solve_batch(args.variant, args.N, *[inst[k][:cores] for k in keys],
-                     mu=inst['mu'][:cores], nthreads=cores)   # warm (thread pool)
-    # chunks of the rank-0 shard in order, wrapping round (further passes over
-    # the same instances) until the budget is spent; parity on the first pass
-    n, done, du, el = 0, 0, 0.0, 0.0
     B = len(inst['x_in'])
-    while el < budget_s:
-        lo = done % B
-        sl = slice(lo, min(lo + chunk, B))
-        t0 = time.perf_counter()
-        r = port.solve_batch(args.variant, args.N, *[inst[k][sl] for k in keys], mu=inst['mu'][sl],
-                             nthreads=cores)
-        el += time.perf_counter() - t0
-        if done < B:
-            ok = (r['status'] == 0) & (gpu_status[sl] == 0)
-            if ok.any():
-                du = max(du, float(np.abs(r['u'][ok] - gpu_u[sl][ok]).max()))
-            n = sl.stop
-        done += sl.stop - sl.start
-    base = {'value': done / el, 'unit': 'QP solves/s', 'cores': cores, 'kind': 'port',
-            'sample': f'{done} solves = {done / B:.1f} passes over the {B}-instance rank-0 shard '
-                      f'in {el:.1f} s; C restatement of the reference gen_dt_dynamics/build_qp + '
-                      f'exact dense dual active-set solve (oracle/hmpc_port.c, OpenMP, '
-                      f'{cores} threads)'}
-    parity = {'instances': n, 'max_abs_du_vs_port': du}
+
+    def leg(threads, seconds, check):
+        chunk = 64 * threads
+        port.solve_batch(args.variant, args.N, *[inst[k][:threads] for k in keys], mu=inst['mu'][:threads],
+                         nthreads=threads)   # warm (thread pool)
+        done, el = 0, 0.0
+        du, mism, n = 0.0, {}, 0
+        while el < seconds:
+            lo = done % B
+            sl = slice(lo, min(lo + chunk, B))
+            t0 = time.perf_counter()
+            r = port.solve_batch(args.variant, args.N, *[inst[k][sl] for k in keys], mu=inst['mu'][sl],
+                                 nthreads=threads)
+            el += time.perf_counter() - t0
+            if check and done < B:
+                gs, ps = gpu_status[sl], r['status']
+                ok = (ps == 0) & (gs == 0)
+                if ok.any():
+                    du = max(du, float(np.abs(r['u'][ok] - gpu_u[sl][ok]).max()))
+                for a, b in zip(gs[gs != ps], ps[gs != ps]):
+                    key = f'{int(a)},{int(b)}'
+                    mism[key] = mism.get(key, 0) + 1
+                n = sl.stop
+            done += sl.stop - sl.start
+        return done, el, du, mism, n
+
+    threads = cpu_threads()
+    d_all, e_all, du, mism, n = leg(threads, 0.75 * budget_s, True)
+    d_one, e_one, _, _, _ = leg(1, 0.25 * budget_s, False)
+    base = {'value': d_all / e_all, 'unit': 'QP solves/s', 'cores': threads, 'kind': 'port',
+            'sample': f'{d_all} solves = {d_all / B:.2f} passes over the {B}-instance rank-0 shard in '
+                      f'{e_all:.1f} s on {threads} threads (this process\'s CPU share; the host reports '
+                      f'os.cpu_count() = {os.cpu_count()}); C restatement of the reference '
+                      f'gen_dt_dynamics/build_qp + exact dense dual active-set solve '
+                      f'(oracle/hmpc_port.c, OpenMP)',
+            'one_core': {'value': d_one / e_one, 'cores': 1,
+                         'sample': f'{d_one} solves in {e_one:.1f} s, 1 thread'},
+            'host_cpu_count': os.cpu_count()}
+    parity = {'instances': n, 'max_abs_du_vs_port': du,
+              'status_mismatch': mism, 'status_mismatch_total': int(sum(mism.values())),
+              'note': 'max_abs_du over instances both solve; status_mismatch keys are '
+                      '"gpu_status,port_status" (0 solved, 1 max_iter, 2 primal_infeasible, 3 numerical)'}
     return base, parity
 
 
@@ -123,28 +195,35 @@ def main():
         raise SystemExit('bench.py needs an MI355X (torch.cuda.is_available() is False)')
     torch.cuda.set_device(local)
     dev = torch.device('cuda', local)
+    backend = None
     if world > 1:
         dist.init_process_group('nccl', device_id=dev)
+        backend = dist.get_backend()
+        assert dist.get_world_size() == world, (dist.get_world_size(), world)
 
     import hmpc
+    import hmpc_dist
     import hmpc_plan
-    from oracle import hmpc_oracle as ho   # constants only (Runner values)
 
-    N, B = args.N, args.batch
+    N = args.N
+    if args.global_batch:
+        start, B = hmpc_dist.strong_shard(args.global_batch, world, rank)
+    else:
+        B = args.batch
+        start = hmpc_dist.shard_start(rank, B)
     inst = hmpc_plan.sample_instances(B, N, curve=not args.straight, seed=args.seed,
-                                      mu_sweep=(0.3, 1.2) if args.mu_sweep else None,
-                                      start=rank * B)   # hmpc_dist.shard_start
+                                      mu_sweep=(0.3, 1.2) if args.mu_sweep else None, start=start)
     d = {k: torch.from_numpy(np.ascontiguousarray(inst[k])).to(dev)
          for k in ('x_in', 'x_lin', 'x_ref', 'pf', 'C', 'mu')}
-    c = ho.runner_constants()
+    c = hmpc_plan.runner_constants()
     ctx = hmpc.Context(args.variant, N, t=c['t'], m=c['m'], g=c['g'], mu=1.0, Jinv=c['Jinv'],
                        rh=c['rh'], device=local, precision=args.precision)
+    kernel = ctx.kernel_name
     out = dict(u=torch.empty((B, N, 6), dtype=torch.float64, device=dev),
                x=torch.empty((B, N + 1, 12), dtype=torch.float64, device=dev),
                obj=torch.empty(B, dtype=torch.float64, device=dev),
                status=torch.empty(B, dtype=torch.int32, device=dev),
                iters=torch.empty(B, dtype=torch.int32, device=dev))
-    import hmpc_dist
     stream = torch.cuda.current_stream(dev)
     # N > 1: the exchange step (per-instance cost + status) is one
     # all-gather of a packed [obj | status] slot on a side stream, pipelined
@@ -182,6 +261,8 @@ def main():
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
+    # solve time on the launch stream (HIP events around hmpc_solve_batch:
+    # the solve kernel + the overflow pass)
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
     tt = torch.tensor([el, kern_ms], dtype=torch.float64, device=dev)
     if world > 1:
@@ -194,6 +275,16 @@ def main():
     sf = torch.tensor([solved_local], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(sf, op=dist.ReduceOp.MIN)
+    dist_info = None
+    if world > 1:
+        ex.wait()
+        torch.cuda.synchronize(dev)
+        if backend == 'nccl':
+            # the RCCL path is the one taken: one all_gather_into_tensor per step
+            assert ex.calls['all_gather_into_tensor'] == args.warmup + args.steps, ex.calls
+            assert ex.calls['all_gather_list'] == 0, ex.calls
+        dist_info = {'world_size': dist.get_world_size(), 'backend': backend,
+                     'exchange_calls': ex.calls, 'exchange_bytes_per_rank_per_step': 12 * B}
 
     base = parity = None
     if rank == 0 and world == 1:
@@ -202,15 +293,16 @@ def main():
     if rank == 0:
         bpsolve = algorithmic_bytes(N)
         achieved = bpsolve * B / (kern_ms * 1e-3) / 1e9
-        traffic = None
-        flops = None
-        tpath = os.path.join(ROOT, 'profiles', 'traffic.json')
+        iters_mean = float(it.mean())
+        flops = algorithmic_flops(kernel, N, iters_mean, min(iters_mean, 6 * N))
+        traffic = executed = None
         wl = f'{args.variant}_N{N}_B{B}_{"straight" if args.straight else "curve"}' \
              f'{"_musweep" if args.mu_sweep else ""}'
-        if os.path.exists(tpath) and args.precision == 'f64':
-            tj = json.load(open(tpath))
-            traffic = tj.get(wl, {}).get('bytes_per_launch')
-            flops = tj.get(wl, {}).get('fp64_flops_per_solve')
+        tpath = os.path.join(ROOT, 'profiles', 'traffic.json')
+        tj = json.load(open(tpath)).get(wl, {}) if os.path.exists(tpath) else {}
+        if tj.get('kernel') == kernel:
+            traffic = tj.get('bytes_per_launch_x2_corrected')
+            executed = tj.get('fp64_flops_executed_per_solve')
         total = B * world * args.steps
         rec = {
             'metric': METRIC,
@@ -221,33 +313,34 @@ def main():
             'warmup': args.warmup,
             'ms_per_step': el / args.steps * 1e3,
             'higher_is_better': True,
-            'scaling': 'weak',
+            'scaling': 'strong' if args.global_batch else 'weak',
             'vs_baseline': None,
             'dtype': 'f32' if args.precision == 'f32' else 'f64',
-            'data': 'synthetic: Runner path_plan_init plan (--curve) + randomised x0 '
-                    '(SURVEY.md 8d), generated on host, resident in HBM before timing',
-            'config': {'workload': f'configs[2]: batch={B}/GPU randomised x0 + '
-                                   f'{"straight" if args.straight else "--curve"} ref traj, '
-                                   f'{args.variant}, horizon N={N}, fp64'
-                                   f'{", mu sweep" if args.mu_sweep else ""}'
-                                   f'{"" if args.precision == "f64" else ", " + args.precision + " (generic kernel)"}',
-                       'global_batch': B * world, 'horizon': N, 'variant': args.variant,
-                       'parallelism': f'shard{world}'},
+            'data': 'synthetic: Runner path_plan_init plan + randomised x0 (SURVEY.md 8d), generated on '
+                    'host, resident in HBM before timing',
+            'config': {'workload': workload_label(args, world), 'global_batch': B * world
+                       if not args.global_batch else args.global_batch, 'per_gpu_batch': B,
+                       'horizon': N, 'variant': args.variant,
+                       'plan': 'straight' if args.straight else 'curve', 'mu_sweep': args.mu_sweep,
+                       'precision': args.precision, 'parallelism': f'shard{world}'},
             'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS,
                          'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic,
-                         'kernel': (f'hmpc::solve_kernel<{args.variant[0]}, {N}>' if args.precision == 'f64' else f'hmpc::wide_kernel<{args.variant[0]}, {"float" if args.precision == "f32" else "double"}>'),
-                         'kernel_ms': kern_ms, 'kernel_ms_max_rank': kern_ms_max,
-                         'algorithmic_bytes_per_solve': bpsolve, 'solves_per_launch': B},
-            # the bound that matters for this path: executed fp64
-            # VALU flops (rocprofv3 SQ_INSTS_VALU_*_F64 x 64 lanes, profiles/)
-            'fp64_vector': None if flops is None else {
+                         'kernel': kernel, 'kernel_ms': kern_ms, 'kernel_ms_max_rank': kern_ms_max,
+                         'algorithmic_bytes_per_solve': bpsolve, 'solves_per_launch': B,
+                         'traffic_note': 'HBM bytes per launch from profiles/traffic.json (rocprofv3 '
+                                         'FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md), null '
+                                         'when no profile of this workload and kernel'},
+            # the bound that matters for this path: fp64 VALU
+            'fp64_vector': {
                 'achieved': flops * B / (kern_ms * 1e-3) / 1e12, 'peak': FP64_VECTOR_PEAK_TFS,
                 'unit': 'TFLOP/s', 'frac': flops * B / (kern_ms * 1e-3) / 1e12 / FP64_VECTOR_PEAK_TFS,
-                'flops_per_solve': flops},
+                'flops_per_solve': flops, 'basis': 'algorithmic (bench.algorithmic_flops, DESIGN.md 5)',
+                'executed_flops_per_solve': executed},
             'cpu_baseline': base,
             'solved_frac_min_rank': float(sf[0]),
-            'iters_mean': float(it.mean()), 'iters_max': int(it.max()),
+            'iters_mean': iters_mean, 'iters_max': int(it.max()),
             'parity_sample': parity,
+            'dist': dist_info,
         }
         print(json.dumps(rec), flush=True)
     if world > 1:

@@ -250,6 +250,27 @@ int hmpc_destroy(hmpc_ctx* c) {
 
 const char* hmpc_last_error(hmpc_ctx* c) { return c ? c->err.c_str() : ""; }
 
+const char* hmpc_kernel_name(hmpc_ctx* c) {
+  if (!c) return "";
+  const bool v3 = c->variant == HMPC_VARIANT_3F;
+  switch (hmpc::pick_kernel(c->variant, c->N, c->precision)) {
+    case hmpc::Kernel::Dense: {
+      static const char* names[2][3] = {
+          {"hmpc::solve_kernel<2, 5>", "hmpc::solve_kernel<2, 10>", "hmpc::solve_kernel<2, 20>"},
+          {"hmpc::solve_kernel<3, 5>", "hmpc::solve_kernel<3, 10>", "hmpc::solve_kernel<3, 20>"}};
+      const int i = c->N == 5 ? 0 : (c->N == 10 ? 1 : 2);
+      return names[v3][i];
+    }
+    case hmpc::Kernel::Riccati:
+      return v3 ? "hmpc::ric_kernel<3>" : "hmpc::ric_kernel<2>";
+    case hmpc::Kernel::Wide:
+      if (c->precision == HMPC_PREC_F32) return v3 ? "hmpc::wide_kernel<3, float>" : "hmpc::wide_kernel<2, float>";
+      return v3 ? "hmpc::wide_kernel<3, double>" : "hmpc::wide_kernel<2, double>";
+    default:
+      return "";
+  }
+}
+
 int hmpc_set_precision(hmpc_ctx* c, int precision) {
   if (!c) return HMPC_ERR_ARG;
   if (precision != HMPC_PREC_F64 && precision != HMPC_PREC_F32 && precision != HMPC_PREC_F64_GENERIC &&

@@ -47,6 +47,7 @@ SIGNATURES = {
     'hmpc_convert_batch': (ctypes.c_int, [_VP, ctypes.c_int64, _VP, _VP, _VP]),
     'hmpc_set_precision': (ctypes.c_int, [_VP, ctypes.c_int]),
     'hmpc_last_error': (ctypes.c_char_p, [_VP]),
+    'hmpc_kernel_name': (ctypes.c_char_p, [_VP]),
     'hmpc_time_solve_batch': (ctypes.c_int, [_VP, ctypes.c_int64] + [_VP] * 11
                               + [ctypes.c_int, _VP, ctypes.POINTER(ctypes.c_double)]),
 }
@@ -92,6 +93,36 @@ class HmpcError(RuntimeError):
     pass
 
 
+def _check_tensor(t, shape, name, device, dtype='float64', optional=False):
+    """A device argument must be a contiguous CUDA tensor of exactly this
+    shape and dtype on the context's device: the C ABI takes raw pointers, so
+    anything else would be an out-of-bounds access or a silent misread."""
+    import torch
+    if t is None:
+        if optional:
+            return
+        raise ValueError(f'{name} is required')
+    dt = torch.float64 if dtype == 'float64' else torch.int32
+    if not isinstance(t, torch.Tensor) or not t.is_cuda:
+        raise ValueError(f'{name} must be a CUDA tensor')
+    if t.device.index != device:
+        raise ValueError(f'{name} is on cuda:{t.device.index}, the context on cuda:{device}')
+    if t.dtype != dt:
+        raise ValueError(f'{name} must be {dtype}, got {t.dtype}')
+    if tuple(t.shape) != tuple(shape):
+        raise ValueError(f'{name} must have shape {tuple(shape)}, got {tuple(t.shape)}')
+    if not t.is_contiguous():
+        raise ValueError(f'{name} must be contiguous')
+
+
+def _check_out(out, B, N, device, need_x=False):
+    _check_tensor(out.get('u'), (B, N, 6), "out['u']", device)
+    _check_tensor(out.get('x'), (B, N + 1, 12), "out['x']", device, optional=not need_x)
+    _check_tensor(out.get('obj'), (B,), "out['obj']", device, optional=True)
+    _check_tensor(out.get('status'), (B,), "out['status']", device, dtype='int32')
+    _check_tensor(out.get('iters'), (B,), "out['iters']", device, dtype='int32', optional=True)
+
+
 class Context:
     """One device-side ``Mpc`` (src/mpc_cvx_euler_3f.py:12-39) for a fixed
     (variant, N) and the Runner's physical constants."""
@@ -116,6 +147,11 @@ class Context:
         self._lib = lib
         if precision != 'f64':
             self._check(lib.hmpc_set_precision(h, PRECISION[precision]), 'hmpc_set_precision')
+
+    @property
+    def kernel_name(self):
+        """The solve kernel this context runs on (hmpc_kernel_name)."""
+        return self._lib.hmpc_kernel_name(self._h).decode()
 
     def close(self):
         if getattr(self, '_h', None):
@@ -158,11 +194,10 @@ class Context:
         import torch
         N = self.N
         B = x_in.shape[0]
-        for t_, shp in ((x_in, (B, 12)), (x_lin, (B, N + 1, 12)), (x_ref, (B, N, 12)),
-                        (pf, (B, N, 3)), (C, (B, N))):
-            if tuple(t_.shape) != shp or t_.dtype != torch.float64 or not t_.is_cuda \
-                    or not t_.is_contiguous():
-                raise ValueError(f'expected contiguous float64 cuda tensor of shape {shp}')
+        for t_, shp, nm in ((x_in, (B, 12), 'x_in'), (x_lin, (B, N + 1, 12), 'x_lin'),
+                            (x_ref, (B, N, 12), 'x_ref'), (pf, (B, N, 3), 'pf'), (C, (B, N), 'C')):
+            _check_tensor(t_, shp, nm, self.device)
+        _check_tensor(mu, (B,), 'mu', self.device, optional=True)
         if out is None:
             dev = x_in.device
             out = dict(u=torch.empty((B, N, 6), dtype=torch.float64, device=dev),
@@ -170,6 +205,7 @@ class Context:
                        obj=torch.empty(B, dtype=torch.float64, device=dev),
                        status=torch.empty(B, dtype=torch.int32, device=dev),
                        iters=torch.empty(B, dtype=torch.int32, device=dev))
+        _check_out(out, B, N, self.device)
         s = stream if stream is not None else torch.cuda.current_stream(x_in.device).cuda_stream
         rc = self._lib.hmpc_solve_batch(self._h, B, _ptr(x_in), _ptr(x_lin), _ptr(x_ref), _ptr(pf),
                                         _ptr(C), _ptr(mu), _ptr(out['u']), _ptr(out.get('x')),
@@ -184,12 +220,17 @@ class Context:
         import torch
         N = self.N
         B = x_in.shape[0]
+        for t_, shp, nm in ((x_in, (B, 12), 'x_in'), (x_ref, (B, N, 12), 'x_ref'), (pf, (B, N, 3), 'pf'),
+                            (C, (B, N), 'C'), (x_prev, (B, N + 1, 12), 'x_prev')):
+            _check_tensor(t_, shp, nm, self.device)
+        _check_tensor(mu, (B,), 'mu', self.device, optional=True)
         if out is None:
             dev = x_in.device
             out = dict(u=torch.empty((B, N, 6), dtype=torch.float64, device=dev),
                        obj=torch.empty(B, dtype=torch.float64, device=dev),
                        status=torch.empty(B, dtype=torch.int32, device=dev),
                        iters=torch.empty(B, dtype=torch.int32, device=dev))
+        _check_out(out, B, N, self.device)
         s = stream if stream is not None else torch.cuda.current_stream(x_in.device).cuda_stream
         rc = self._lib.hmpc_mpcontrol_batch(self._h, B, 1 if init else 0, _ptr(x_in), _ptr(x_ref),
                                             _ptr(pf), _ptr(C), _ptr(mu), _ptr(x_prev),
@@ -217,6 +258,12 @@ class Context:
                                  'or (B,T,12)/(B,T,3)')
         if not shared and x_ref_plan.shape[0] != B:
             raise ValueError('per-robot plans need a leading batch dimension B')
+        for t_, nm in ((x_ref_plan, 'x_ref_plan'), (pf_plan, 'pf_plan')):
+            _check_tensor(t_, tuple(t_.shape), nm, self.device)
+        _check_tensor(x_in, (B, 12), 'x_in', self.device)
+        _check_tensor(x_prev, (B, N + 1, 12), 'x_prev', self.device)
+        _check_tensor(C, (N,) if C.dim() == 1 else (B, N), 'C', self.device)
+        _check_tensor(mu, (B,), 'mu', self.device, optional=True)
         C_bs = 0 if C.dim() == 1 else N
         if out is None:
             dev = x_in.device
@@ -224,6 +271,7 @@ class Context:
                        obj=torch.empty(B, dtype=torch.float64, device=dev),
                        status=torch.empty(B, dtype=torch.int32, device=dev),
                        iters=torch.empty(B, dtype=torch.int32, device=dev))
+        _check_out(out, B, N, self.device)
         s = stream if stream is not None else torch.cuda.current_stream(x_in.device).cuda_stream
         rc = self._lib.hmpc_mpcontrol_plan_batch(
             self._h, B, 1 if init else 0, _ptr(x_in), _ptr(x_ref_plan), _ptr(pf_plan), T,
@@ -239,9 +287,15 @@ class Context:
         in place; see hmpc_plant_batch for the strides."""
         import torch
         B = X.shape[0]
-        if tuple(X.shape) != (B, 13) or X.dtype != torch.float64 or not X.is_cuda \
-                or not X.is_contiguous():
-            raise ValueError('X must be a contiguous float64 cuda tensor (B,13)')
+        _check_tensor(X, (B, 13), 'X', self.device)
+        for t_, nm in ((U, 'U'), (pf, 'pf')):
+            _check_tensor(t_, tuple(t_.shape), nm, self.device)
+        if U.numel() < (B - 1) * int(U_bstride) + 6:
+            raise ValueError('U is too small for B rows at U_bstride')
+        if pf.numel() < (B - 1) * int(pf_bstride) + (int(n_steps) - 1) * int(pf_sstride) + 3:
+            raise ValueError('pf is too small for B robots x n_steps at the given strides')
+        _check_tensor(X_hist, (B, int(n_steps), 13), 'X_hist', self.device, optional=True)
+        _check_tensor(x_out, (B, 12), 'x_out', self.device, optional=True)
         Jh = np.ascontiguousarray(np.asarray(J, dtype=np.float64).reshape(9))
         s = stream if stream is not None else torch.cuda.current_stream(X.device).cuda_stream
         rc = self._lib.hmpc_plant_batch(self._h, B, int(n_steps), float(dt), Jh.ctypes.data_as(_D),
@@ -253,6 +307,8 @@ class Context:
     def convert_device(self, X, x, stream=None):
         """x (B,12) = convert(X (B,13)) (src/robotrunner.py:19-28)."""
         import torch
+        _check_tensor(X, (X.shape[0], 13), 'X', self.device)
+        _check_tensor(x, (X.shape[0], 12), 'x', self.device)
         s = stream if stream is not None else torch.cuda.current_stream(X.device).cuda_stream
         rc = self._lib.hmpc_convert_batch(self._h, X.shape[0], _ptr(X), _ptr(x), ctypes.c_void_p(s))
         self._check(rc, 'hmpc_convert_batch')
@@ -260,6 +316,12 @@ class Context:
     def time_solve_device(self, x_in, x_lin, x_ref, pf, C, mu, out, reps, stream):
         """Mean kernel time (ms) over `reps` back-to-back launches, measured
         with HIP events on `stream` inside the library."""
+        B, N = x_in.shape[0], self.N
+        for t_, shp, nm in ((x_in, (B, 12), 'x_in'), (x_lin, (B, N + 1, 12), 'x_lin'),
+                            (x_ref, (B, N, 12), 'x_ref'), (pf, (B, N, 3), 'pf'), (C, (B, N), 'C')):
+            _check_tensor(t_, shp, nm, self.device)
+        _check_tensor(mu, (B,), 'mu', self.device, optional=True)
+        _check_out(out, B, N, self.device)
         ms = ctypes.c_double()
         rc = self._lib.hmpc_time_solve_batch(self._h, x_in.shape[0], _ptr(x_in), _ptr(x_lin),
                                              _ptr(x_ref), _ptr(pf), _ptr(C), _ptr(mu),

@@ -18,6 +18,16 @@ def shard_start(rank: int, per_rank: int) -> int:
     return rank * per_rank
 
 
+def strong_shard(global_batch: int, world: int, rank: int):
+    """(start, count) of rank's contiguous shard of a fixed global batch
+    (strong scaling, BASELINE configs[3]: 262144 instances over 2/4/8 GPUs);
+    the first global_batch % world ranks take one instance more."""
+    base, extra = divmod(global_batch, world)
+    count = base + (1 if rank < extra else 0)
+    start = rank * base + min(rank, extra)
+    return start, count
+
+
 def allgather_results(obj: torch.Tensor, status: torch.Tensor, out_obj=None, out_status=None):
     """Concatenate every rank's (obj, status) in rank order on every rank."""
     world = dist.get_world_size()
@@ -61,6 +71,11 @@ class ResultExchange:
         self.stream = torch.cuda.Stream(self.device) if self.cuda else None
         self.done = [None] * nslots
         self.k = 0
+        # which collective ran, by path (checked by bench.py and the tests:
+        # on the nccl (= RCCL) backend the exchange must be the one
+        # all_gather_into_tensor, never the list fallback)
+        self.backend = dist.get_backend()
+        self.calls = {'all_gather_into_tensor': 0, 'all_gather_list': 0}
 
     def outputs(self):
         """(obj float64 [n], status int32 [n]) views of the next slot's send
@@ -89,9 +104,11 @@ class ResultExchange:
         return s
 
     def _gather(self, s):
-        if dist.get_backend() == 'nccl':
+        if self.backend == 'nccl':
             dist.all_gather_into_tensor(self.recv[s], self.send[s])
+            self.calls['all_gather_into_tensor'] += 1
         else:
+            self.calls['all_gather_list'] += 1
             dist.all_gather(list(self.recv[s].view(self.world, 12 * self.n).unbind(0)),
                             self.send[s])
 

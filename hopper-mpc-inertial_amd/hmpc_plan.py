@@ -50,6 +50,17 @@ class RunnerConfig:
         return 0.4 * (self.N_run * self.dt)
 
 
+def runner_constants():
+    """Physical constants the Runner hands to ``Mpc`` (src/robotrunner.py:37-48,
+    68, 76): m, g, the MPC step t = mpc_dt, mu, the body inertia J and its
+    inverse, and the hip offset rh."""
+    J = np.array([[76148072.89, 70089.52, 2067970.36],
+                  [70089.52, 45477183.53, -87045.58],
+                  [2067970.36, -87045.58, 76287220.47]]) * (10 ** (-9))   # :38-40
+    return dict(t=0.02, m=7.5, g=9.807, mu=1.0, J=J, Jinv=np.linalg.inv(J),
+                rh=-np.array([0.02663114, 0.04435752, 6.61082088]) / 1000)   # :43
+
+
 def gait_scheduler(cfg: RunnerConfig, t, t0):
     phi = np.mod((t - t0) / cfg.t_p, 1)
     return 0 if phi > cfg.phi_switch else 1

@@ -39,12 +39,11 @@ class Runner:
         self.dyn = dyn
         self.B = int(batch)
         self.device = torch.device('cuda', device)
-        m, g = 7.5, 9.807                                                       # :37,44
-        self.J = np.array([[76148072.89, 70089.52, 2067970.36],
-                           [70089.52, 45477183.53, -87045.58],
-                           [2067970.36, -87045.58, 76287220.47]]) * (10 ** (-9))  # :38-40
-        self.Jinv = np.linalg.inv(self.J)
-        self.rh = -np.array([0.02663114, 0.04435752, 6.61082088]) / 1000       # :43
+        c = hp.runner_constants()                                              # :37-48
+        m, g = c['m'], c['g']
+        self.J = c['J']
+        self.Jinv = c['Jinv']
+        self.rh = c['rh']
         self.ctx = hmpc.Context(dyn, N, t=self.cfg.mpc_dt, m=m, g=g, mu=mu, Jinv=self.Jinv,
                                 rh=self.rh, uref_mode=uref_mode, device=device)
         X0 = X0_DEFAULT if X0 is None else np.asarray(X0, dtype=np.float64)

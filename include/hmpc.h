@@ -176,6 +176,11 @@ int hmpc_convert_batch(hmpc_ctx* ctx, int64_t B, const double* X, double* x, voi
    (reduced Hessian condition ~3e6), see DESIGN.md. */
 int hmpc_set_precision(hmpc_ctx* ctx, int precision);
 
+/* Name of the solve kernel this context's (variant, N, precision) runs on,
+   e.g. "hmpc::solve_kernel<3, 10>" or "hmpc::ric_kernel<3>" (static string;
+   "" when none).  For benchmark records and profiles. */
+const char* hmpc_kernel_name(hmpc_ctx* ctx);
+
 /* Last HIP error string of this context ("" if none). */
 const char* hmpc_last_error(hmpc_ctx* ctx);
 

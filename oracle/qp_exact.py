@@ -17,7 +17,8 @@ kernel (which condenses and runs a dual active-set method):
    stationarity residual all below 1e-9 (scaled).
 
 Status strings: 'solved' (certificate holds), 'solved_inaccurate' (IPM only),
-'primal_infeasible', 'failed'.
+'primal_infeasible' (certified: the LP min_violation -- the least t with
+l - t <= A z <= u + t -- is > 1e-7), 'failed' (no convergence, no certificate).
 """
 from __future__ import annotations
 
@@ -49,15 +50,22 @@ def _kkt_solve(Hs, E, rhs_x, rhs_e):
     return sol[:n], sol[n:], lu
 
 
-def ipm(P, q, E, e, G, g, tol=1e-12, max_iter=120):
+def ipm(P, q, E, e, G, g, tol=1e-12, max_iter=200):
     n, me, mi = P.shape[0], E.shape[0], G.shape[0]
     Ps = sp.csr_matrix(P)
     Gs = sp.csr_matrix(G)
-    z = np.zeros(n)
-    y = np.zeros(me)
-    s = np.ones(mi)
+    # initial point: the equality-constrained optimum (inequalities dropped),
+    # slacks max(g - G z, 1), unit multipliers.  (A cold start from z = 0
+    # diverges on the Runner's N = 60 run at its last call, where x_in sits
+    # ~1 m above the plan.)
+    try:
+        z, y, _ = _kkt_solve((Ps + 1e-9 * sp.eye(n)).tocsc(), E, -q, e)
+    except RuntimeError:
+        z, y = np.zeros(n), np.zeros(me)
+    if not np.all(np.isfinite(z)):
+        z, y = np.zeros(n), np.zeros(me)
+    s = np.maximum(g - Gs @ z, 1.0)
     lam = np.ones(mi)
-    # initial point: solve equality QP with slack-regularised inequalities
     for it in range(max_iter):
         rd = Ps @ z + q + E.T @ y + Gs.T @ lam
         re = E @ z - e
@@ -106,7 +114,31 @@ def ipm(P, q, E, e, G, g, tol=1e-12, max_iter=120):
     with np.errstate(all='ignore'):
         rp = max(np.abs(E @ z - e).max(initial=0), np.maximum(Gs @ z - g, 0).max(initial=0))
     bad = not np.isfinite(rp) or rp > 1e-6
-    return z, y, s, lam, ('primal_infeasible' if bad else 'solved_inaccurate'), it
+    return z, y, s, lam, ('failed' if bad else 'solved_inaccurate'), it
+
+
+def min_violation(A, l, u):
+    """Certificate of (in)feasibility of l <= A z <= u: the LP
+    min t  s.t.  l - t <= A z <= u + t,  t >= 0  (scipy HiGHS).  Returns
+    (t*, z): t* = 0 (to the LP's tolerance) with a feasible z, or t* > 0 --
+    no point violates every row by less than t*, i.e. the QP is primal
+    infeasible."""
+    from scipy.optimize import linprog
+    A = np.asarray(A, dtype=np.float64)
+    m, n = A.shape
+    rows, rhs = [], []
+    fu, fl = np.isfinite(u), np.isfinite(l)
+    # A z - t <= u ;  -A z - t <= -l
+    Au = np.hstack([A[fu], -np.ones((fu.sum(), 1))])
+    Al = np.hstack([-A[fl], -np.ones((fl.sum(), 1))])
+    c = np.zeros(n + 1)
+    c[-1] = 1.0
+    res = linprog(c, A_ub=sp.vstack([sp.csr_matrix(Au), sp.csr_matrix(Al)]),
+                  b_ub=np.concatenate([u[fu], -l[fl]]),
+                  bounds=[(None, None)] * n + [(0, None)], method='highs')
+    if res.status != 0:
+        return np.nan, None
+    return float(res.x[-1]), res.x[:n]
 
 
 def _polish(P, q, E, e, G, g, active, refine=6, delta=1e-11):
@@ -150,8 +182,11 @@ def solve(P, q, A, l, u, tol=1e-9, max_repair=20):
     u = np.asarray(u, dtype=np.float64)
     E, e, G, g, src = _split(A, l, u)
     z, y, s, lam, st, its = ipm(P, q, E, e, G, g)
-    if st == 'primal_infeasible':
-        return dict(x=None, y=None, status=st, cert=None, iters=its)
+    if st == 'failed':
+        # no convergence: primal_infeasible only with a certificate
+        t, _ = min_violation(A, l, u)
+        st = 'primal_infeasible' if (np.isfinite(t) and t > 1e-7) else 'failed'
+        return dict(x=None, y=None, status=st, cert=None, iters=its, min_violation=t)
     best = (z, y, lam, certificate(P, q, E, e, G, g, z, y, lam), 'solved_inaccurate')
     active = lam > s
     for rep in range(max_repair):

@@ -258,4 +258,4 @@ if __name__ == '__main__':
         make_qp_fixture('3f', 10, True, 16, 2, seed=6, mu_sweep=(0.3, 1.2))
     if 'loop' in which:
         make_closed_loop_fixture(10, 1000, False, 'loop_3f_N10.npz', n_detail=50)
-        make_closed_loop_fixture(60, 2000, False, 'loop_3f_N60_config1.npz', n_detail=2)
+        make_closed_loop_fixture(60, 2000, False, 'loop_3f_N60_config1.npz', n_detail=100)

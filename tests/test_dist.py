@@ -53,7 +53,14 @@ def _worker(rank, world, port, q):
         slots.append(ex.exchange())
     ex.wait()
     po, ps = ex.results(slots[2])   # slot 0 again: step 2 overwrote step 0
-    q.put((rank, oa.numpy().copy(), sa.numpy().copy(), po.numpy().copy() / 3, ps.numpy().copy() - 2))
+    # gloo takes the list all-gather; the nccl (RCCL) path is counted apart
+    assert ex.backend == 'gloo'
+    assert ex.calls == {'all_gather_into_tensor': 0, 'all_gather_list': 3}, ex.calls
+    # strong scaling: a fixed global batch in contiguous shards
+    gstart, gcount = hmpc_dist.strong_shard(2 * PER_RANK + 1, world, rank)
+    sobj, sst = _solve(gstart, gcount)
+    q.put((rank, oa.numpy().copy(), sa.numpy().copy(), po.numpy().copy() / 3, ps.numpy().copy() - 2,
+           gstart, gcount, sobj, sst))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -73,8 +80,16 @@ def test_sharded_allgather_equals_single_process(world):
         p.join(timeout=60)
         assert p.exitcode == 0
     obj_ref, st_ref = _solve(0, PER_RANK * world)
-    for _, oa, sa, po, ps in res:
+    for _, oa, sa, po, ps, *_ in res:
         assert np.array_equal(oa, obj_ref)
         assert np.array_equal(sa, st_ref)
         assert np.allclose(po, obj_ref, rtol=1e-15, atol=0)
         assert np.array_equal(ps, st_ref)
+    # the strong-scaling shards tile [0, 2 PER_RANK + 1) and reproduce the
+    # single-process solve bit for bit
+    gobj, gst = _solve(0, 2 * PER_RANK + 1)
+    shards = sorted((r[5], r[6], r[7], r[8]) for r in res)
+    assert shards[0][0] == 0 and shards[0][0] + shards[0][1] == shards[1][0]
+    assert shards[1][0] + shards[1][1] == 2 * PER_RANK + 1
+    assert np.array_equal(np.concatenate([sh[2] for sh in shards]), gobj)
+    assert np.array_equal(np.concatenate([sh[3] for sh in shards]), gst)

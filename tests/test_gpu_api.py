@@ -1,0 +1,71 @@
+"""Host-side argument checks of the device entry points (hmpc.py): every
+tensor handed to the C ABI as a raw pointer is validated first (shape, dtype,
+device, contiguity), so a wrong tensor raises instead of becoming an
+out-of-bounds GPU access; and the library reports which kernel serves a
+context (hmpc_kernel_name)."""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip('torch')
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope='module')
+def hm():
+    if not torch.cuda.is_available():
+        pytest.fail('GPU tests need an MI355X (torch.cuda.is_available() is False)')
+    import hmpc
+    return hmpc
+
+
+def make(hm, N=10, precision='f64'):
+    import hmpc_plan
+    c = hmpc_plan.runner_constants()
+    return hm.Context('3f', N, t=c['t'], m=c['m'], g=c['g'], mu=1.0, Jinv=c['Jinv'], rh=c['rh'],
+                      precision=precision)
+
+
+def inputs(N, B=4):
+    import hmpc_plan
+    inst = hmpc_plan.sample_instances(B, N, curve=True, seed=5)
+    return {k: torch.from_numpy(np.ascontiguousarray(inst[k])).cuda()
+            for k in ('x_in', 'x_lin', 'x_ref', 'pf', 'C', 'mu')}
+
+
+def test_bad_tensors_raise(hm):
+    N = 10
+    cx = make(hm, N)
+    d = inputs(N)
+    args = [d[k] for k in ('x_in', 'x_lin', 'x_ref', 'pf', 'C')]
+    cx.solve_device(*args, mu=d['mu'])   # the good call
+    bad = [
+        (1, d['x_lin'].float()),                  # dtype
+        (2, d['x_ref'][:, :N - 1].contiguous()),   # shape
+        (3, d['pf'].cpu()),                       # device
+        (0, d['x_in'].t().contiguous().t()),      # (shape differs too)
+    ]
+    for i, t in bad:
+        a = list(args)
+        a[i] = t
+        with pytest.raises(ValueError):
+            cx.solve_device(*a, mu=d['mu'])
+    with pytest.raises(ValueError):
+        cx.solve_device(*args, mu=d['mu'][:2])
+    out = dict(u=torch.empty((4, N, 6), dtype=torch.float64, device='cuda'),
+               status=torch.empty(4, dtype=torch.int64, device='cuda'))   # wrong status dtype
+    with pytest.raises(ValueError):
+        cx.solve_device(*args, mu=d['mu'], out=out)
+    x_prev = torch.empty((4, N, 12), dtype=torch.float64, device='cuda')   # one row short
+    with pytest.raises(ValueError):
+        cx.mpcontrol_device(False, d['x_in'], d['x_ref'], d['pf'], d['C'], x_prev)
+    cx.close()
+
+
+def test_kernel_names(hm):
+    assert make(hm, 10).kernel_name == 'hmpc::solve_kernel<3, 10>'
+    assert make(hm, 20).kernel_name == 'hmpc::ric_kernel<3>'
+    assert make(hm, 60).kernel_name == 'hmpc::ric_kernel<3>'
+    assert make(hm, 10, 'f64_riccati').kernel_name == 'hmpc::ric_kernel<3>'
+    assert make(hm, 20, 'f64_dense').kernel_name == 'hmpc::solve_kernel<3, 20>'
+    assert make(hm, 10, 'f64_generic').kernel_name == 'hmpc::wide_kernel<3, double>'

@@ -9,7 +9,7 @@ pinned bit for bit to the reference's own build_qp) is
     l <= A z <= u -- a feasible point certifies the QP is feasible;
   * solved by oracle/qp_exact (IPM + polish + KKT certificate).
 
-Writes the per-solve inputs to tests/golden/loop_3f_N60_inputs.npz when
+Writes the per-solve inputs to gpurun_out/loop_3f_N60_inputs.npz (scratch) when
 --save is given.
 """
 import os
@@ -65,7 +65,8 @@ def violation(qp, z):
 
 
 def main():
-    save = '--save' in sys.argv
+    save = "--save" in sys.argv
+    only_last = "--last" in sys.argv
     N = 60
     orig = ho.OracleMpc
     holder = {}
@@ -105,7 +106,7 @@ def main():
     if save:
         arrs = {k: np.array([s[k] for s in log]) for k in ('x_in', 'x_lin', 'x_ref', 'pf', 'C', 'u', 'x',
                                                            'obj', 'status')}
-        np.savez_compressed(os.path.join(ROOT, 'tests', 'golden', 'loop_3f_N60_inputs.npz'), **arrs)
+        np.savez_compressed(os.path.join(ROOT, "gpurun_out", "loop_3f_N60_inputs.npz"), **arrs)
 
 
 if __name__ == '__main__':
