@@ -1,0 +1,120 @@
+"""The active-set capacity cliff is gone: instances whose optimal active set
+is larger than the main kernel's capacity (dense N = 10 kernel: 20 in
+registers; Riccati kernel: ric_qcap(N) in LDS -- 40 at N <= 32, 64 beyond)
+are handed to the overflow pass (capacity 6N, R in global memory) and come
+back solved, equal to the C port, instead of HMPC_NUMERICAL.
+
+Adversarial instances: mu = 0.3 and large start-state errors (angular rates
++-20..30 rad/s, horizontal velocity +-3..5 m/s) saturate the torque box and
+the friction pyramid over most stages.  The active-set size at the optimum is
+counted on the CPU from the port's solution against the reference-form
+constraint rows (oracle/hmpc_oracle.build_qp), so the test proves the cases
+really exceed the capacities it claims to cover.
+"""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip('torch')
+
+pytestmark = pytest.mark.gpu
+
+U_TOL = 1e-6
+
+
+@pytest.fixture(scope='module')
+def hm():
+    if not torch.cuda.is_available():
+        pytest.fail('GPU tests need an MI355X (torch.cuda.is_available() is False)')
+    import hmpc
+    return hmpc
+
+
+def adversarial(B, N, seed, wscale, vscale, mu=0.3):
+    import hmpc_plan as hp
+    inst = hp.sample_instances(B, N, curve=True, seed=seed, mu_sweep=(mu, mu))
+    rng = np.random.default_rng(seed)
+    inst['x_in'][:, 9:12] += rng.choice([-1, 1], (B, 3)) * rng.uniform(0.7, 1.0, (B, 3)) * wscale
+    inst['x_in'][:, 6:8] += rng.choice([-1, 1], (B, 2)) * rng.uniform(0.7, 1.0, (B, 2)) * vscale
+    inst['x_in'][:, 3:5] += rng.uniform(-0.4, 0.4, (B, 2))
+    inst['x_lin'][:, 0] = inst['x_in']
+    return inst
+
+
+def active_rows(N, inst, ref, i):
+    """Inequality rows of the reference-built QP active at the port's optimum."""
+    from oracle import hmpc_oracle as ho
+    p = ho.MpcParams.runner('3f', N, mu=float(inst['mu'][i]))
+    _, _, Gd = ho.constant_matrices(p)
+    Ad, Bd = ho.gen_dt_dynamics(p, inst['x_lin'][i], inst['pf'][i])
+    qp = ho.build_qp(p, inst['x_in'][i], inst['x_ref'][i], Ad, Bd, Gd, inst['C'][i])
+    z = np.concatenate([ref['x'][i].ravel(), ref['u'][i].ravel()])
+    Az = qp['A'] @ z
+    ineq = qp['l'] != qp['u']
+    act = ineq & ((np.abs(Az - qp['l']) < 1e-7) | (np.abs(Az - qp['u']) < 1e-7))
+    return int(act.sum())
+
+
+def solve_both(hm, N, inst, precision):
+    import hmpc_plan
+    from oracle import port
+    c = hmpc_plan.runner_constants()
+    cx = hm.Context('3f', N, t=c['t'], m=c['m'], g=c['g'], mu=1.0, Jinv=c['Jinv'], rh=c['rh'],
+                    precision=precision)
+    gpu = cx.solve_host(inst['x_in'], inst['x_lin'], inst['x_ref'], inst['pf'], inst['C'], mu=inst['mu'])
+    kernel = cx.kernel_name
+    cx.close()
+    ref = port.solve_batch('3f', N, inst['x_in'], inst['x_lin'], inst['x_ref'], inst['pf'], inst['C'],
+                           mu=inst['mu'], nthreads=16)
+    return gpu, ref, kernel
+
+
+@pytest.mark.parametrize('precision,kernel,cap', [('f64', 'hmpc::solve_kernel<3, 10>', 20),
+                                                  ('f64_riccati', 'hmpc::ric_kernel<3>', 40)])
+def test_overflow_n10(hm, precision, kernel, cap):
+    N, B = 10, 48
+    inst = adversarial(B, N, 2, 30.0, 5.0)
+    gpu, ref, k = solve_both(hm, N, inst, precision)
+    assert k == kernel
+    assert (ref['status'] == 0).all()
+    assert np.array_equal(gpu['status'], ref['status'])
+    assert np.abs(gpu['u'] - ref['u']).max() <= U_TOL
+    nact = [active_rows(N, inst, ref, i) for i in range(B)]
+    assert max(nact) > cap, nact
+
+
+def test_overflow_n60(hm):
+    N, B = 60, 24
+    inst = adversarial(B, N, 2, 12.0, 2.0)
+    gpu, ref, k = solve_both(hm, N, inst, 'f64')
+    assert k == 'hmpc::ric_kernel<3>'
+    assert (ref['status'] == 0).all()
+    assert np.array_equal(gpu['status'], ref['status'])
+    assert np.abs(gpu['u'] - ref['u']).max() <= U_TOL
+    nact = [active_rows(N, inst, ref, i) for i in range(8)]
+    assert max(nact) > 64, nact
+
+
+def test_overflow_mpcontrol_shift_in_place(hm):
+    """mpcontrol's time-shift pass reads x_prev and writes x* into the same
+    buffer: an overflowed instance's main pass must leave x_prev intact for
+    the overflow pass.  Two calls (init, then shift) against the drop-in
+    replay with host-side linearisation."""
+    import hmpc_plan
+    N, B = 10, 16
+    inst = adversarial(B, N, 3, 30.0, 5.0)
+    c = hmpc_plan.runner_constants()
+    cx = hm.Context('3f', N, t=c['t'], m=c['m'], g=c['g'], mu=1.0, Jinv=c['Jinv'], rh=c['rh'])
+    d = {k: torch.from_numpy(np.ascontiguousarray(inst[k])).cuda()
+         for k in ('x_in', 'x_ref', 'pf', 'C', 'mu')}
+    xp = torch.zeros((B, N + 1, 12), dtype=torch.float64, device='cuda')
+    o1 = cx.mpcontrol_device(True, d['x_in'], d['x_ref'], d['pf'], d['C'], xp, mu=d['mu'])
+    x1 = xp.clone()
+    o2 = cx.mpcontrol_device(False, d['x_in'], d['x_ref'], d['pf'], d['C'], xp, mu=d['mu'])
+    torch.cuda.synchronize()
+    assert (o1['status'] == 0).all() and (o2['status'] == 0).all()
+    # the same second solve from the host: linearisation = time shift of x1
+    x_lin = torch.cat([d['x_in'][:, None], x1[:, 2:], x1[:, -1:]], dim=1).cpu().numpy()
+    r = cx.solve_host(inst['x_in'], x_lin, inst['x_ref'], inst['pf'], inst['C'], mu=inst['mu'])
+    cx.close()
+    assert np.array_equal(r['status'], o2['status'].cpu().numpy())
+    np.testing.assert_array_equal(r['u'], o2['u'].cpu().numpy())
