@@ -165,6 +165,7 @@ __device__ void ric_solve(const SolveArgs& a, const int N, const int64_t b, doub
   double* ua = sm + L.UA;
   int* act = reinterpret_cast<int*>(sm + L.ACT);
   double* gv = sm + L.GV;
+  double* cbv = sm + L.CB;
   double* sdg = sm + L.SD;
   double* un = sm + L.U0;
 
@@ -797,15 +798,21 @@ __device__ void ric_solve(const SolveArgs& a, const int N, const int64_t b, doub
       const double* zsrc = sv;
       double zn = sn;
       if (q > 0) {
+        // r to LDS first: the per-stage loop below runs on lanes < N only,
+        // and a readlane from a lane outside it would read a stale register
+#pragma unroll
+        for (int e = 0; e < ENT; ++e) {
+          const int ai = 64 * e + lane;
+          if (ai < q) cbv[ai] = rv[e];
+        }
+        rsync();
         for (int j = lane; j < N; j += RT) {
           double acc[6] = {0, 0, 0, 0, 0, 0};
           add_coef(p, j, 1.0, acc);
-          for (int ai = 0; ai < q; ++ai) add_coef(act[ai], j, -vget(rv, ai), acc);
+          for (int ai = 0; ai < q; ++ai) add_coef(act[ai], j, -cbv[ai], acc);
 #pragma unroll
           for (int c = 0; c < 6; ++c) nb[6 * j + c] = acc[c];
         }
-        // (the vget above is wave-uniform: every lane runs the same trip count
-        // when N <= 64)
         rsync();
         hinv(zv);
         zsrc = zv;
