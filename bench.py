@@ -297,7 +297,8 @@ def main():
         flops = algorithmic_flops(kernel, N, iters_mean, min(iters_mean, 6 * N))
         traffic = executed = None
         wl = f'{args.variant}_N{N}_B{B}_{"straight" if args.straight else "curve"}' \
-             f'{"_musweep" if args.mu_sweep else ""}'
+             f'{"_musweep" if args.mu_sweep else ""}' \
+             f'{"" if args.precision == "f64" else "_" + args.precision}'
         tpath = os.path.join(ROOT, 'profiles', 'traffic.json')
         tj = json.load(open(tpath)).get(wl, {}) if os.path.exists(tpath) else {}
         if tj.get('kernel') == kernel:
@@ -325,6 +326,7 @@ def main():
                        'precision': args.precision, 'parallelism': f'shard{world}'},
             'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS,
                          'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic,
+                         'traffic_over_algorithmic': traffic / (bpsolve * B) if traffic else None,
                          'kernel': kernel, 'kernel_ms': kern_ms, 'kernel_ms_max_rank': kern_ms_max,
                          'algorithmic_bytes_per_solve': bpsolve, 'solves_per_launch': B,
                          'traffic_note': 'HBM bytes per launch from profiles/traffic.json (rocprofv3 '

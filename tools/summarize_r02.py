@@ -82,7 +82,8 @@ def main(tag, cfgs):
                                                'algorithmic': alg,
                                                'x2_corrected_over_algorithmic': (2 * fetch + write) / alg}
             c = bench['config']
-            wl = f"{c['variant']}_N{c['horizon']}_B{B}_{c['plan']}{'_musweep' if c['mu_sweep'] else ''}"
+            wl = f"{c['variant']}_N{c['horizon']}_B{B}_{c['plan']}{'_musweep' if c['mu_sweep'] else ''}" \
+                 f"{'' if c['precision'] == 'f64' else '_' + c['precision']}"
             tj[wl] = {'kernel': kernel, 'bytes_per_launch_x2_corrected': 2 * fetch + write,
                       'bytes_per_launch_raw': fetch + write, 'fetch_bytes_raw': fetch, 'write_bytes': write,
                       'fp64_flops_executed_per_solve': f64 / B,
