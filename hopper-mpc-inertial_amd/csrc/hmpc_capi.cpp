@@ -250,6 +250,22 @@ int hmpc_destroy(hmpc_ctx* c) {
 
 const char* hmpc_last_error(hmpc_ctx* c) { return c ? c->err.c_str() : ""; }
 
+int hmpc_active_capacity(hmpc_ctx* c) {
+  if (!c) return -1;
+  switch (hmpc::pick_kernel(c->variant, c->N, c->precision)) {
+    case hmpc::Kernel::Dense: {
+      const int nv = 6 * c->N, q = c->N <= 10 ? 20 : 48;
+      return nv < 20 ? nv : q;   // QMAX of hmpc_kernels.hip
+    }
+    case hmpc::Kernel::Riccati:
+      return hmpc::ric_qcap(c->N);
+    case hmpc::Kernel::Wide:
+      return 0;
+    default:
+      return -1;
+  }
+}
+
 const char* hmpc_kernel_name(hmpc_ctx* c) {
   if (!c) return "";
   const bool v3 = c->variant == HMPC_VARIANT_3F;
@@ -262,7 +278,8 @@ const char* hmpc_kernel_name(hmpc_ctx* c) {
       return names[v3][i];
     }
     case hmpc::Kernel::Riccati:
-      return v3 ? "hmpc::ric_kernel<3>" : "hmpc::ric_kernel<2>";
+      if (hmpc::ric_occ(c->N) == 2) return v3 ? "hmpc::ric_kernel<3, 2>" : "hmpc::ric_kernel<2, 2>";
+      return v3 ? "hmpc::ric_kernel<3, 1>" : "hmpc::ric_kernel<2, 1>";
     case hmpc::Kernel::Wide:
       if (c->precision == HMPC_PREC_F32) return v3 ? "hmpc::wide_kernel<3, float>" : "hmpc::wide_kernel<2, float>";
       return v3 ? "hmpc::wide_kernel<3, double>" : "hmpc::wide_kernel<2, double>";

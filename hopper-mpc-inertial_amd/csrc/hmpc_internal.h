@@ -66,11 +66,13 @@ constexpr int kRicNmax = 64;
 constexpr int kDenseNmax = 10;
 constexpr int ST_OVERFLOW = 4;   // internal: re-solved by the overflow pass
 // LDS capacity of R for the main pass at horizon N
-inline int ric_qcap(int N) {
-  const int nv = 6 * N;
-  const int cap = N <= 32 ? 40 : 64;
-  return nv < cap ? nv : cap;
-}
+// Active-set capacity of the main Riccati kernel's LDS-resident R and its
+// occupancy (waves per SIMD): the largest capacity <= min(64, 6N) whose LDS
+// fits 8 workgroups per CU (2 waves / SIMD, the register budget compiled into
+// ric_kernel<VAR, 2>) with capacity >= 32, else 4 workgroups per CU (1 wave /
+// SIMD).  Larger active sets go to the overflow pass.
+int ric_qcap(int N);
+int ric_occ(int N);
 // dynamic LDS bytes of the Riccati kernel at horizon N (R in LDS with
 // capacity qcap, or none when qcap == 0: overflow pass)
 size_t ric_lds_bytes(int N, int qcap);

@@ -27,7 +27,7 @@
 // z_k = free response + sum_{j<=k-2} dt (dt/m)(k-1-j) fz_j); swing and 2f fy
 // equalities (:134-136, 2f :129) are fixed variables (zero columns of B_k).
 //
-// R lives in LDS with a capacity ric_qcap(N); an instance whose active set
+// R lives in LDS with a capacity ric_qcap(N) (hmpc_internal.h); an instance whose active set
 // outgrows it is handed to the overflow pass (capacity 6N, R in global
 // memory) instead of failing.
 #include <hip/hip_runtime.h>
@@ -46,7 +46,7 @@ constexpr int RT = 64;   // one wavefront per workgroup
 // LDS layout (in doubles) for a runtime horizon N and active-set capacity cap
 // (R in LDS only when r_lds).
 struct RicLay {
-  int XIN, CC, CS, BW, ZB, ZN, ZD, MISC, VV, SV, ZV, NB, MU, UA, ACT, CB, GV, SD, RM, U0, total;
+  int XIN, CC, CS, BW, ZB, ZN, ZD, MISC, VV, SV, NB, ZV, MU, UA, ACT, CB, SD, RM, U0, total;
   __host__ __device__ RicLay(int N, int cap, bool r_lds) {
     const int NV = 6 * N;
     auto up2 = [](int x) { return (x + 1) & ~1; };   // 16-B alignment of every array
@@ -61,16 +61,14 @@ struct RicLay {
     MISC = o; o += 8;
     VV = o; o += NV;              // primal iterate
     SV = o; o += NV;              // s = H^-1 n_p
-    ZV = o; o += NV;              // z = H^-1 (n_p - N_A r)
     NB = o; o += NV;              // right-hand side of H^-1 (n_p, n_p - N_A r)
+    ZV = o; o += NV;              // z = H^-1 (n_p - N_A r); with MU: d_t (12 N) in phase 1
     MU = o; o += NV;              // sweep scratch (mu, then G^-1 mu)
     UA = o; o = up2(o + cap);     // active multipliers
     ACT = o; o = up2(o + cap);    // active ids (int)
-    CB = o; o = up2(o + cap);     // scratch
-    GV = o; o += 2 * up2(cap);    // Givens of a drop
-    SD = o; o = up2(o + cap);     // subdiagonal scratch
-    U0 = o;                       // union: x_ref (12N) | Riccati scratch (568)
-    o += (12 * N > 568 ? 12 * N : 568);
+    CB = o; o = up2(o + cap);     // r of the dual step (z builder), then the
+    SD = CB;                      // subdiagonal of a drop (not live together)
+    U0 = o; o += 568;             // Riccati scratch
     RM = o; if (r_lds) o = up2(o + cap * (cap + 1) / 2);   // packed upper R
     total = o;
   }
@@ -140,7 +138,7 @@ __device__ __forceinline__ void vset(double (&v)[ENT], int i, double x) {
   for (int e = 0; e < ENT; ++e) v[e] = (64 * e + lane == i) ? x : v[e];
 }
 
-template <int VAR, int ENT>
+template <int VAR, int ENT, int RING>
 __device__ void ric_solve(const SolveArgs& a, const int N, const int64_t b, double* sm, double* Rm,
                           const int cap, double* kw) {
   const RicLay L(N, cap, false);
@@ -164,7 +162,6 @@ __device__ void ric_solve(const SolveArgs& a, const int N, const int64_t b, doub
   double* gi = kw + 72 * N;   // G_k^-1 (global workspace)
   double* ua = sm + L.UA;
   int* act = reinterpret_cast<int*>(sm + L.ACT);
-  double* gv = sm + L.GV;
   double* cbv = sm + L.CB;
   double* sdg = sm + L.SD;
   double* un = sm + L.U0;
@@ -180,10 +177,6 @@ __device__ void ric_solve(const SolveArgs& a, const int N, const int64_t b, doub
   const double* xrf = a.x_ref + b * a.xref_bs;
   const double mu = a.mu ? a.mu[b] : a.mu_default;
   if (lane < 12) xin[lane] = a.x_in[b * 12 + lane];
-  for (int i = lane; i < 12 * N; i += RT) {
-    const int r = i / 12, c = i - 12 * r;
-    un[i] = xrf[(int64_t)r * a.xref_rs + c];
-  }
   for (int k = lane; k < N; k += RT) {
     cc[k] = a.C[b * a.C_bs + k];
     const double* row;
@@ -201,22 +194,23 @@ __device__ void ric_solve(const SolveArgs& a, const int N, const int64_t b, doub
   RS_ACC(0, t_p0);
   RS_T(t_p1);
   // ---------------- phase 1: free response, d_t, adjoint, gradient ----------
-  // lane r < 12 holds component r.  d_t = kf Q (xbar_t - r_{t-1}) overwrites
-  // x_ref row t-1; the gradient h = 2 Gamma' W (xbar - r) - 2 V ubar goes to
+  // lane r < 12 holds component r.  d_t = kf Q (xbar_t - r_{t-1}) goes to
+  // ZV..MU (12 N, free until phase 3); the gradient h = 2 Gamma' W (xbar - r) - 2 V ubar goes to
   // NB as -h (the right-hand side of the unconstrained optimum).
   {
+    double* dd = zv;
     double xr = lane < 12 ? xin[lane] : 0.0;
     const double qr = qdiag(lane);
     if (lane == 2) zb[0] = xr;
     for (int k = 0; k < N; ++k) {
       xr = ad_lane(xr, dt, cs[2 * k], cs[2 * k + 1]) + ((lane == 8) ? -a.g * dt : 0.0);
       const double kf = (k == N - 1) ? kTermQ : 1.0;
-      if (lane < 12) un[12 * k + lane] = kf * qr * (xr - un[12 * k + lane]);
+      if (lane < 12) dd[12 * k + lane] = kf * qr * (xr - xrf[(int64_t)k * a.xref_rs + lane]);
       if (lane == 2) zb[k + 1] = xr;
     }
     wsync();
     const double ubar_alias = (cc[N - 1] != 0.0) ? 2.0 * a.m * a.g : 0.0;
-    double ar = lane < 12 ? un[12 * (N - 1) + lane] : 0.0;   // a_N = d_N
+    double ar = lane < 12 ? dd[12 * (N - 1) + lane] : 0.0;   // a_N = d_N
     for (int t = N; t >= 1; --t) {
       const int i = t - 1;
       const double a6 = rdlane(ar, 6), a7 = rdlane(ar, 7), a8 = rdlane(ar, 8);
@@ -239,7 +233,7 @@ __device__ void ric_solve(const SolveArgs& a, const int N, const int64_t b, doub
         nb[6 * i + c] = -h;
       }
       if (t >= 2) {
-        ar = adt_lane(ar, dt, cs[2 * i], cs[2 * i + 1]) + (lane < 12 ? un[12 * (t - 2) + lane] : 0.0);
+        ar = adt_lane(ar, dt, cs[2 * i], cs[2 * i + 1]) + (lane < 12 ? dd[12 * (t - 2) + lane] : 0.0);
       }
     }
   }
@@ -518,18 +512,30 @@ __device__ void ric_solve(const SolveArgs& a, const int N, const int64_t b, doub
       };
       // (loads are unconditional -- out-of-range steps reload stage 0 -- so
       // that the vmcnt/lgkmcnt waits stay counted, not drained)
-      BwdL R0, R1, R2;
-      load_b(N - 1, R0);
-      load_b(N >= 2 ? N - 2 : 0, R1);
-      for (int j = N - 1; j >= 0; j -= 3) {
-        load_b(j >= 2 ? j - 2 : 0, R2);
-        bstep(j, R0);
-        if (j < 1) break;
-        load_b(j >= 3 ? j - 3 : 0, R0);
-        bstep(j - 1, R1);
-        if (j < 2) break;
-        load_b(j >= 4 ? j - 4 : 0, R1);
-        bstep(j - 2, R2);
+      if constexpr (RING == 3) {
+        BwdL R0, R1, R2;
+        load_b(N - 1, R0);
+        load_b(N >= 2 ? N - 2 : 0, R1);
+        for (int j = N - 1; j >= 0; j -= 3) {
+          load_b(j >= 2 ? j - 2 : 0, R2);
+          bstep(j, R0);
+          if (j < 1) break;
+          load_b(j >= 3 ? j - 3 : 0, R0);
+          bstep(j - 1, R1);
+          if (j < 2) break;
+          load_b(j >= 4 ? j - 4 : 0, R1);
+          bstep(j - 2, R2);
+        }
+      } else {   // two-deep (register budget of 2 waves / SIMD)
+        BwdL R0, R1;
+        load_b(N - 1, R0);
+        for (int j = N - 1; j >= 0; j -= 2) {
+          load_b(j >= 1 ? j - 1 : 0, R1);
+          bstep(j, R0);
+          if (j < 1) break;
+          load_b(j >= 2 ? j - 2 : 0, R0);
+          bstep(j - 1, R1);
+        }
       }
     }
     wsync();
@@ -594,18 +600,30 @@ __device__ void ric_solve(const SolveArgs& a, const int N, const int64_t b, doub
         b2 = fma(r5, u5, b2);
         xi = lane < 12 ? (b0 + b1) + b2 : 0.0;
       };
-      FwdL R0, R1, R2;
-      load_f(0, R0);
-      load_f(N >= 2 ? 1 : 0, R1);
-      for (int k = 0; k < N; k += 3) {
-        load_f(k + 2 < N ? k + 2 : N - 1, R2);
-        fstep(k, R0);
-        if (k + 1 >= N) break;
-        load_f(k + 3 < N ? k + 3 : N - 1, R0);
-        fstep(k + 1, R1);
-        if (k + 2 >= N) break;
-        load_f(k + 4 < N ? k + 4 : N - 1, R1);
-        fstep(k + 2, R2);
+      if constexpr (RING == 3) {
+        FwdL R0, R1, R2;
+        load_f(0, R0);
+        load_f(N >= 2 ? 1 : 0, R1);
+        for (int k = 0; k < N; k += 3) {
+          load_f(k + 2 < N ? k + 2 : N - 1, R2);
+          fstep(k, R0);
+          if (k + 1 >= N) break;
+          load_f(k + 3 < N ? k + 3 : N - 1, R0);
+          fstep(k + 1, R1);
+          if (k + 2 >= N) break;
+          load_f(k + 4 < N ? k + 4 : N - 1, R1);
+          fstep(k + 2, R2);
+        }
+      } else {
+        FwdL R0, R1;
+        load_f(0, R0);
+        for (int k = 0; k < N; k += 2) {
+          load_f(k + 1 < N ? k + 1 : N - 1, R1);
+          fstep(k, R0);
+          if (k + 1 >= N) break;
+          load_f(k + 2 < N ? k + 2 : N - 1, R0);
+          fstep(k + 1, R1);
+        }
       }
     }
     wsync();
@@ -926,11 +944,7 @@ __device__ void ric_solve(const SolveArgs& a, const int N, const int64_t b, doub
     }
     return;
   }
-  // x_ref again (its LDS copy is gone) into the union, x* staged over SV..
-  for (int i = lane; i < 12 * N; i += RT) {
-    const int r = i / 12, c = i - 12 * r;
-    un[i] = xrf[(int64_t)r * a.xref_rs + c];
-  }
+  // x* staged over SV.. (x_ref read from global in the objective)
   for (int i = lane; i < NV; i += RT) {
     const int j = i / 6, c = i - 6 * j;
     const bool fr = c >= 3 || (cc[j] != 0.0 && !(VAR == 2 && c == 1));
@@ -939,7 +953,7 @@ __device__ void ric_solve(const SolveArgs& a, const int N, const int64_t b, doub
     a.u[b * NV + i] = u;
   }
   wsync();
-  double* xo = sv;   // 12 (N+1) <= 4 NV doubles (SV, ZV, NB, MU)
+  double* xo = sv;   // 12 (N+1) <= 4 NV doubles (SV, NB, ZV, MU)
   {
     double xr = lane < 12 ? xin[lane] : 0.0;
     if (lane < 12) xo[lane] = xr;
@@ -960,7 +974,7 @@ __device__ void ric_solve(const SolveArgs& a, const int N, const int64_t b, doub
       }
       xr = lane < 12 ? nx : 0.0;
       const double kf = (k == N - 1) ? kTermQ : 1.0;
-      const double e = lane < 12 ? xr - un[12 * k + lane] : 0.0;
+      const double e = lane < 12 ? xr - xrf[(int64_t)k * a.xref_rs + lane] : 0.0;
       objl = fma(kf * qr * e, e, objl);
       if (k < N - 1 && lane < 6) {
         const double ub = a.uref_aliased ? ub_alias : ((cc[k] != 0.0) ? 2.0 * a.m * a.g : 0.0);
@@ -991,8 +1005,10 @@ __device__ void ric_solve(const SolveArgs& a, const int N, const int64_t b, doub
 // Persistent: a.ric_groups workgroups, each with its slot of the K / G^-1
 // workspace, take instances off an atomic counter (a.work, zeroed with the
 // overflow count before the launch) until the batch is done.
-template <int VAR>
-__global__ void __launch_bounds__(RT) ric_kernel(SolveArgs a, int N, int cap) {
+// OCC = waves per SIMD the register allocation is held to (2: <= 256 VGPRs +
+// AGPRs; 1: up to 512)
+template <int VAR, int OCC>
+__global__ void __launch_bounds__(RT) __attribute__((amdgpu_waves_per_eu(OCC, OCC))) ric_kernel(SolveArgs a, int N, int cap) {
   extern __shared__ __attribute__((aligned(16))) double ric_sm[];
   const RicLay L(N, cap, true);
   double* kw = a.kws + (int64_t)blockIdx.x * a.kws_stride;
@@ -1001,7 +1017,7 @@ __global__ void __launch_bounds__(RT) ric_kernel(SolveArgs a, int N, int cap) {
     if (threadIdx.x == 0) b = atomicAdd(a.work, 1);
     b = __builtin_amdgcn_readfirstlane(b);
     if (b >= a.B) break;
-    ric_solve<VAR, 1>(a, N, (int64_t)b, ric_sm, ric_sm + L.RM, cap, kw);
+    ric_solve<VAR, 1, OCC == 2 ? 2 : 3>(a, N, (int64_t)b, ric_sm, ric_sm + L.RM, cap, kw);
     __syncthreads();
   }
 }
@@ -1018,7 +1034,7 @@ __global__ void __launch_bounds__(RT) ric_overflow_kernel(SolveArgs a, int N) {
   a2.ovf_count = nullptr;   // no further overflow: capacity is 6N
   for (int i = blockIdx.x; i < n; i += gridDim.x) {
     const int64_t b = a.ovf_list[i];
-    ric_solve<VAR, (6 * kRicNmax + 63) / 64>(a2, N, b, ric_sm, Rm, 6 * N, kw);
+    ric_solve<VAR, (6 * kRicNmax + 63) / 64, 3>(a2, N, b, ric_sm, Rm, 6 * N, kw);
     __syncthreads();
   }
 }
@@ -1037,6 +1053,25 @@ size_t ric_lds_bytes(int N, int qcap) {
   return (size_t)L.total * sizeof(double);
 }
 
+namespace {
+constexpr size_t kLdsPerCU = 160 * 1024;
+struct RicCfg {
+  int cap, occ;
+};
+RicCfg ric_config(int N) {
+  const int nv = 6 * N, cmax = nv < 64 ? nv : 64, cmin = nv < 32 ? nv : 32;
+  for (int occ = 2; occ >= 1; --occ) {
+    const size_t budget = kLdsPerCU / (4 * occ);
+    for (int c = cmax; c >= cmin; --c)
+      if (ric_lds_bytes(N, c) <= budget) return {c, occ};
+  }
+  return {cmin, 1};
+}
+}  // namespace
+
+int ric_qcap(int N) { return ric_config(N).cap; }
+int ric_occ(int N) { return ric_config(N).occ; }
+
 int64_t ric_kws_stride(int N) { return ric_kws_doubles(N); }
 
 int64_t ric_rws_stride(int N) {
@@ -1044,21 +1079,30 @@ int64_t ric_rws_stride(int N) {
   return (((nv * (nv + 1) / 2) + 15) & ~(int64_t)15) + ric_kws_doubles(N);
 }
 
-int ric_groups(int variant, int N) {
+namespace {
+template <int VAR, int OCC>
+bool ric_launch(int N, const SolveArgs& a, hipStream_t s, int* per) {
   const int cap = ric_qcap(N);
   const size_t lds = ric_lds_bytes(N, cap);
+  if (!set_lds(ric_kernel<VAR, OCC>, lds)) return false;
+  if (per) return hipOccupancyMaxActiveBlocksPerMultiprocessor(per, ric_kernel<VAR, OCC>, RT, lds) == hipSuccess;
+  const unsigned g = (unsigned)(a.B < a.ric_groups ? a.B : a.ric_groups);
+  hipLaunchKernelGGL((ric_kernel<VAR, OCC>), dim3(g), dim3(RT), lds, s, a, N, cap);
+  return true;
+}
+bool ric_launch_any(int variant, int N, const SolveArgs& a, hipStream_t s, int* per) {
+  const bool o2 = ric_occ(N) == 2;
+  if (variant == 3) return o2 ? ric_launch<3, 2>(N, a, s, per) : ric_launch<3, 1>(N, a, s, per);
+  return o2 ? ric_launch<2, 2>(N, a, s, per) : ric_launch<2, 1>(N, a, s, per);
+}
+}  // namespace
+
+int ric_groups(int variant, int N) {
   int dev = 0, cus = 0, per = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
-  hipError_t e;
-  if (variant == 3) {
-    if (!set_lds(ric_kernel<3>, lds)) return 0;
-    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, ric_kernel<3>, RT, lds);
-  } else {
-    if (!set_lds(ric_kernel<2>, lds)) return 0;
-    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, ric_kernel<2>, RT, lds);
-  }
-  if (e != hipSuccess || per < 1) per = 1;
+  SolveArgs none{};
+  if (!ric_launch_any(variant, N, none, nullptr, &per) || per < 1) per = 1;
   return cus * per;
 }
 
@@ -1066,17 +1110,7 @@ bool launch_solve_ric(int variant, int N, const SolveArgs& a, hipStream_t s) {
   if (N < 1 || N > kRicNmax || (variant != 2 && variant != 3)) return false;
   if (a.B <= 0) return true;
   if (!a.work || !a.kws || a.ric_groups < 1) return false;
-  const int cap = ric_qcap(N);
-  const size_t lds = ric_lds_bytes(N, cap);
-  const unsigned g = (unsigned)(a.B < a.ric_groups ? a.B : a.ric_groups);
-  if (variant == 3) {
-    if (!set_lds(ric_kernel<3>, lds)) return false;
-    hipLaunchKernelGGL(ric_kernel<3>, dim3(g), dim3(RT), lds, s, a, N, cap);
-  } else {
-    if (!set_lds(ric_kernel<2>, lds)) return false;
-    hipLaunchKernelGGL(ric_kernel<2>, dim3(g), dim3(RT), lds, s, a, N, cap);
-  }
-  return true;
+  return ric_launch_any(variant, N, a, s, nullptr);
 }
 
 bool launch_solve_ric_overflow(int variant, int N, const SolveArgs& a, int groups, hipStream_t s) {

@@ -48,6 +48,7 @@ SIGNATURES = {
     'hmpc_set_precision': (ctypes.c_int, [_VP, ctypes.c_int]),
     'hmpc_last_error': (ctypes.c_char_p, [_VP]),
     'hmpc_kernel_name': (ctypes.c_char_p, [_VP]),
+    'hmpc_active_capacity': (ctypes.c_int, [_VP]),
     'hmpc_time_solve_batch': (ctypes.c_int, [_VP, ctypes.c_int64] + [_VP] * 11
                               + [ctypes.c_int, _VP, ctypes.POINTER(ctypes.c_double)]),
 }
@@ -152,6 +153,11 @@ class Context:
     def kernel_name(self):
         """The solve kernel this context runs on (hmpc_kernel_name)."""
         return self._lib.hmpc_kernel_name(self._h).decode()
+
+    @property
+    def active_capacity(self):
+        """Active-set capacity of the main pass (hmpc_active_capacity)."""
+        return int(self._lib.hmpc_active_capacity(self._h))
 
     def close(self):
         if getattr(self, '_h', None):

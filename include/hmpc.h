@@ -177,9 +177,15 @@ int hmpc_convert_batch(hmpc_ctx* ctx, int64_t B, const double* X, double* x, voi
 int hmpc_set_precision(hmpc_ctx* ctx, int precision);
 
 /* Name of the solve kernel this context's (variant, N, precision) runs on,
-   e.g. "hmpc::solve_kernel<3, 10>" or "hmpc::ric_kernel<3>" (static string;
+   e.g. "hmpc::solve_kernel<3, 10>" or "hmpc::ric_kernel<3, 2>" (static string;
    "" when none).  For benchmark records and profiles. */
 const char* hmpc_kernel_name(hmpc_ctx* ctx);
+
+/* Active-set capacity of that kernel's main pass (-1 when none): instances
+   whose active set grows beyond it are re-solved by the overflow pass
+   (capacity 6N) inside the same call, so this is a performance figure, not a
+   limit (0 for the generic kernel, which has no overflow pass). */
+int hmpc_active_capacity(hmpc_ctx* ctx);
 
 /* Last HIP error string of this context ("" if none). */
 const char* hmpc_last_error(hmpc_ctx* ctx);

@@ -1,11 +1,12 @@
 """The active-set capacity cliff is gone: instances whose optimal active set
-is larger than the main kernel's capacity (dense N = 10 kernel: 20 in
-registers; Riccati kernel: ric_qcap(N) in LDS -- 40 at N <= 32, 64 beyond)
+is larger than the main kernel's capacity (hmpc_active_capacity: dense N = 10
+kernel 20 in registers; Riccati kernel ric_qcap(N) in LDS -- 50 at N = 10,
+47 at N = 60)
 are handed to the overflow pass (capacity 6N, R in global memory) and come
 back solved, equal to the C port, instead of HMPC_NUMERICAL.
 
-Adversarial instances: mu = 0.3 and large start-state errors (angular rates
-+-20..30 rad/s, horizontal velocity +-3..5 m/s) saturate the torque box and
+Adversarial instances: mu = 0.2..0.3 and large start-state errors (angular
+rates +-8..50 rad/s, horizontal velocity +-1.4..8 m/s) saturate the torque box and
 the friction pyramid over most stages.  The active-set size at the optimum is
 counted on the CPU from the port's solution against the reference-form
 constraint rows (oracle/hmpc_oracle.build_qp), so the test proves the cases
@@ -62,18 +63,19 @@ def solve_both(hm, N, inst, precision):
                     precision=precision)
     gpu = cx.solve_host(inst['x_in'], inst['x_lin'], inst['x_ref'], inst['pf'], inst['C'], mu=inst['mu'])
     kernel = cx.kernel_name
+    cap = cx.active_capacity
     cx.close()
     ref = port.solve_batch('3f', N, inst['x_in'], inst['x_lin'], inst['x_ref'], inst['pf'], inst['C'],
                            mu=inst['mu'], nthreads=16)
-    return gpu, ref, kernel
+    return gpu, ref, kernel, cap
 
 
-@pytest.mark.parametrize('precision,kernel,cap', [('f64', 'hmpc::solve_kernel<3, 10>', 20),
-                                                  ('f64_riccati', 'hmpc::ric_kernel<3>', 40)])
-def test_overflow_n10(hm, precision, kernel, cap):
+@pytest.mark.parametrize('precision,kernel', [('f64', 'hmpc::solve_kernel<3, 10>'),
+                                             ('f64_riccati', 'hmpc::ric_kernel<3, 2>')])
+def test_overflow_n10(hm, precision, kernel):
     N, B = 10, 48
-    inst = adversarial(B, N, 2, 30.0, 5.0)
-    gpu, ref, k = solve_both(hm, N, inst, precision)
+    inst = adversarial(B, N, 2, 50.0, 8.0, mu=0.2)   # optimal active sets up to 55 of 60
+    gpu, ref, k, cap = solve_both(hm, N, inst, precision)
     assert k == kernel
     assert (ref['status'] == 0).all()
     assert np.array_equal(gpu['status'], ref['status'])
@@ -85,13 +87,13 @@ def test_overflow_n10(hm, precision, kernel, cap):
 def test_overflow_n60(hm):
     N, B = 60, 24
     inst = adversarial(B, N, 2, 12.0, 2.0)
-    gpu, ref, k = solve_both(hm, N, inst, 'f64')
-    assert k == 'hmpc::ric_kernel<3>'
+    gpu, ref, k, cap = solve_both(hm, N, inst, 'f64')
+    assert k == 'hmpc::ric_kernel<3, 1>'
     assert (ref['status'] == 0).all()
     assert np.array_equal(gpu['status'], ref['status'])
     assert np.abs(gpu['u'] - ref['u']).max() <= U_TOL
     nact = [active_rows(N, inst, ref, i) for i in range(8)]
-    assert max(nact) > 64, nact
+    assert max(nact) > cap, (cap, nact)
 
 
 def test_overflow_mpcontrol_shift_in_place(hm):
