@@ -85,6 +85,17 @@ __host__ __device__ inline int64_t ric_kws_doubles(int N) { return ((93 * (int64
 
 __device__ __forceinline__ int loff(int r) { return (r * (r + 1)) >> 1; }
 
+// maximum over the wave of x in [0, 63] (uniform result), by six ballots
+__device__ __forceinline__ int wave_imax63(int x) {
+  int hi = 0;
+#pragma unroll
+  for (int bit = 5; bit >= 0; --bit) {
+    const int cand = hi | (1 << bit);
+    if (__ballot(x >= cand)) hi = cand;
+  }
+  return hi;
+}
+
 // Ordering point between lanes of the one wavefront of a workgroup: LDS
 // instructions of a wave execute in order, so only the compiler must be kept
 // from reordering them.  Global-memory hand-offs between lanes (the K / G^-1
@@ -475,7 +486,9 @@ __device__ void ric_solve(const SolveArgs& a, const int N, const int64_t b, doub
     for (int c = 0; c < 6; ++c) d.br[c] = bw[18 * k + 6 * rr + c];
     asm volatile("" ::: "memory");   // issue here, two steps ahead of the use
   };
-  auto hinv = [&](double* dst) __attribute__((always_inline)) {
+  // jt (uniform): the last stage where the right-hand side NB is nonzero --
+  // the backward sweep starts there (lam_{jt+1} = 0, mu_j = 0 beyond it)
+  auto hinv = [&](double* dst, int jt) __attribute__((always_inline)) {
     // ---- backward sweep
     {
       double li = 0.0;                                  // lam_{j+1}[lane]
@@ -514,9 +527,9 @@ __device__ void ric_solve(const SolveArgs& a, const int N, const int64_t b, doub
       // that the vmcnt/lgkmcnt waits stay counted, not drained)
       if constexpr (RING == 3) {
         BwdL R0, R1, R2;
-        load_b(N - 1, R0);
-        load_b(N >= 2 ? N - 2 : 0, R1);
-        for (int j = N - 1; j >= 0; j -= 3) {
+        load_b(jt, R0);
+        load_b(jt >= 1 ? jt - 1 : 0, R1);
+        for (int j = jt; j >= 0; j -= 3) {
           load_b(j >= 2 ? j - 2 : 0, R2);
           bstep(j, R0);
           if (j < 1) break;
@@ -528,8 +541,8 @@ __device__ void ric_solve(const SolveArgs& a, const int N, const int64_t b, doub
         }
       } else {   // two-deep (register budget of 2 waves / SIMD)
         BwdL R0, R1;
-        load_b(N - 1, R0);
-        for (int j = N - 1; j >= 0; j -= 2) {
+        load_b(jt, R0);
+        for (int j = jt; j >= 0; j -= 2) {
           load_b(j >= 1 ? j - 1 : 0, R1);
           bstep(j, R0);
           if (j < 1) break;
@@ -538,9 +551,10 @@ __device__ void ric_solve(const SolveArgs& a, const int N, const int64_t b, doub
         }
       }
     }
+    for (int i = 6 * (jt + 1) + lane; i < NV; i += RT) mu_[i] = 0.0;
     wsync();
-    // ---- w_j = G_j^-1 mu_j (lane-per-stage)
-    for (int j = lane; j < N; j += RT) {
+    // ---- w_j = G_j^-1 mu_j (lane-per-stage; 0 beyond jt)
+    for (int j = lane; j <= jt; j += RT) {
       double mv[6], w[6], g[21];
       const double* gj = gi + 21 * j;
 #pragma unroll
@@ -648,7 +662,7 @@ __device__ void ric_solve(const SolveArgs& a, const int N, const int64_t b, doub
   RS_ACC(2, t_p2);
   RS_T(t_p3);
   // ---------------- phase 3: unconstrained optimum v0 = -H^-1 h --------------
-  hinv(vv);
+  hinv(vv, N - 1);
   // |n| of the z rows (lane k): zc sqrt(sum_{j <= k-2, stance} (k-1-j)^2)
   if (lane < N) {
     double s2 = 0.0;
@@ -696,6 +710,12 @@ __device__ void ric_solve(const SolveArgs& a, const int N, const int64_t b, doub
     }
 #pragma unroll
     for (int t = 0; t < 6; ++t) acc[t] = fma(s, e[t], acc[t]);
+  };
+  // last stage a constraint row touches: its own stage k, or k - 2 for the
+  // z row of stage k (fz_j, j <= k - 2)
+  auto stage_top = [](int id) -> int {
+    const int v = id >> 2, k = v / 6, c = v - 6 * k;
+    return (c >= 3 && (id & 3) >= 2) ? k - 2 : k;
   };
   auto rhs_of = [&](int id) -> double {
     const int v = id >> 2, sl = id & 3, k = v / 6, c = v - 6 * k;
@@ -764,7 +784,7 @@ __device__ void ric_solve(const SolveArgs& a, const int N, const int64_t b, doub
       for (int c = 0; c < 6; ++c) nb[6 * j + c] = acc[c];
     }
     rsync();
-    hinv(sv);                     // s = H^-1 n_p
+    hinv(sv, stage_top(p));       // s = H^-1 n_p
     const double sn = vdot(nb, sv);
     const double szd = zdot(sv);
     if (lane < N) zd[lane] = szd;
@@ -832,7 +852,13 @@ __device__ void ric_solve(const SolveArgs& a, const int N, const int64_t b, doub
           for (int c = 0; c < 6; ++c) nb[6 * j + c] = acc[c];
         }
         rsync();
-        hinv(zv);
+        int tz = stage_top(p);   // n_p - N_A r: the last stage of p and the active rows
+#pragma unroll
+        for (int e = 0; e < ENT; ++e) {
+          const int ai = 64 * e + lane;
+          if (ai < q) tz = max(tz, stage_top(act[ai]));
+        }
+        hinv(zv, wave_imax63(tz));
         zsrc = zv;
         zn = vdot(nb, zv);
       }
