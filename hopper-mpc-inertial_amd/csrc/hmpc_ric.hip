@@ -68,14 +68,15 @@ struct RicLay {
     ACT = o; o = up2(o + cap);    // active ids (int)
     CB = o; o = up2(o + cap);     // r of the dual step (z builder), then the
     SD = CB;                      // subdiagonal of a drop (not live together)
-    U0 = o; o += 568;             // Riccati scratch
-    RM = o; if (r_lds) o = up2(o + cap * (cap + 1) / 2);   // packed upper R
-    total = o;
+    U0 = o; o += 568;             // Riccati scratch | x_ref (12 N, phases 0-1 and 5,
+    RM = o; if (r_lds) o = up2(o + cap * (cap + 1) / 2);   // over R too); packed upper R
+    total = o > U0 + 12 * N ? o : U0 + 12 * N;
   }
 };
 
-// Riccati scratch inside the union (P, P A, P B, B'P A, G, Dinv, K_k)
-constexpr int PS_OFF = 0, M1_OFF = 144, TS_OFF = 288, FS_OFF = 360, GS_OFF = 432, DL_OFF = 468,
+// Riccati scratch inside the union (P_{k+1} and P_k in turn, P B, B'P A, G,
+// Dinv, K_k)
+constexpr int PS_OFF = 0, P2_OFF = 144, TS_OFF = 288, FS_OFF = 360, GS_OFF = 432, DL_OFF = 468,
               KL_OFF = 490;
 
 // Global workspace of one workgroup (doubles): K_k [6][12] and G_k^-1 (packed
@@ -150,10 +151,16 @@ __device__ __forceinline__ void vset(double (&v)[ENT], int i, double x) {
 }
 
 template <int VAR, int ENT, int RING>
-__device__ void ric_solve(const SolveArgs& a, const int N, const int64_t b, double* sm, double* Rm,
+__device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, double* sm, double* Rm,
                           const int cap, double* kw) {
+  // lane and N through volatile asm: made afresh for every instance, so the
+  // compiler cannot hoist lane- and N-derived values (masks, offsets) out of
+  // the persistent instance loop and hold them -- spilled -- for the kernel's
+  // whole life
+  int lane, N;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(lane) : "v"((int)threadIdx.x));
+  asm volatile("s_mov_b32 %0, %1" : "=s"(N) : "s"(N_));
   const RicLay L(N, cap, false);
-  const int lane = threadIdx.x;
   const int NV = 6 * N;
   const double dt = a.dt, dtm = dt / a.m;
   const double zc = dt * dtm;   // coefficient scale of fz_j in z_k
@@ -188,6 +195,10 @@ __device__ void ric_solve(const SolveArgs& a, const int N, const int64_t b, doub
   const double* xrf = a.x_ref + b * a.xref_bs;
   const double mu = a.mu ? a.mu[b] : a.mu_default;
   if (lane < 12) xin[lane] = a.x_in[b * 12 + lane];
+  for (int i = lane; i < 12 * N; i += RT) {
+    const int r = i / 12, c = i - 12 * r;
+    un[i] = xrf[(int64_t)r * a.xref_rs + c];
+  }
   for (int k = lane; k < N; k += RT) {
     cc[k] = a.C[b * a.C_bs + k];
     const double* row;
@@ -206,7 +217,7 @@ __device__ void ric_solve(const SolveArgs& a, const int N, const int64_t b, doub
   RS_T(t_p1);
   // ---------------- phase 1: free response, d_t, adjoint, gradient ----------
   // lane r < 12 holds component r.  d_t = kf Q (xbar_t - r_{t-1}) goes to
-  // ZV..MU (12 N, free until phase 3); the gradient h = 2 Gamma' W (xbar - r) - 2 V ubar goes to
+  // ZV..MU (12 N, free until phase 3), x_ref is staged in the union; the gradient h = 2 Gamma' W (xbar - r) - 2 V ubar goes to
   // NB as -h (the right-hand side of the unconstrained optimum).
   {
     double* dd = zv;
@@ -216,7 +227,7 @@ __device__ void ric_solve(const SolveArgs& a, const int N, const int64_t b, doub
     for (int k = 0; k < N; ++k) {
       xr = ad_lane(xr, dt, cs[2 * k], cs[2 * k + 1]) + ((lane == 8) ? -a.g * dt : 0.0);
       const double kf = (k == N - 1) ? kTermQ : 1.0;
-      if (lane < 12) dd[12 * k + lane] = kf * qr * (xr - xrf[(int64_t)k * a.xref_rs + lane]);
+      if (lane < 12) dd[12 * k + lane] = kf * qr * (xr - un[12 * k + lane]);
       if (lane == 2) zb[k + 1] = xr;
     }
     wsync();
@@ -253,71 +264,115 @@ __device__ void ric_solve(const SolveArgs& a, const int N, const int64_t b, doub
   RS_ACC(1, t_p1);
   RS_T(t_p2);
   // ---------------- phase 2: Riccati factorisation -------------------------
+  // P_N = 2 (100 Q); per stage k = N-1..0, with A_k = I + dt E_k (column j of
+  // A_k: 1 at row j plus at most two more rows, arow/acoef below):
+  //   (a) T = P B                      (12 x 6; fixed columns 0)
+  //   (b) G = 2 V + B'T, F = T'A       (identity rows/cols for fixed variables)
+  //   (c) G = D D' (reciprocal pivots), K = G^-1 F, Dinv
+  //   (d) G^-1 = Dinv'Dinv, P_k = 2 Q + A'P A - F'K straight from P_{k+1}
+  //       (no P A product: every entry of A'P A is <= 9 entries of P)
+  // Work items are laid over the 64 lanes with a second item per lane for
+  // the overhang, both in one unrolled body (their LDS latencies overlap).
   int status = ST_SOLVED;
   {
-    double* P = un + PS_OFF;    // P_{k+1}, 12 x 12 full
-    double* M1 = un + M1_OFF;   // P A
+    double* Pc = un + PS_OFF;   // P_{k+1}, 12 x 12 full
+    double* Pn = un + P2_OFF;   // P_k
     double* T = un + TS_OFF;    // P B, 12 x 6
     double* F = un + FS_OFF;    // B'P A, 6 x 12
     double* G = un + GS_OFF;    // 6 x 6
+    double* Dl = un + DL_OFF;   // Dinv, packed lower
+    double* Kl = un + KL_OFF;   // K_k (the P update reads it)
     for (int e = lane; e < 144; e += RT) {
       const int i = e / 12, j = e - 12 * i;
-      P[e] = (i == j) ? 2.0 * kTermQ * kQ[i] : 0.0;
+      Pc[e] = (i == j) ? 2.0 * kTermQ * kQ[i] : 0.0;
     }
+    // lane constants: P-update items (i, j), j <= i (78 = 64 + 14), the G^-1
+    // item (c, d) of lanes < 21
+    auto tri = [](int e, int& i, int& j) {
+      i = 0;
+      while (loff(i + 1) <= e) ++i;
+      j = e - loff(i);
+    };
+    int pi0, pj0, pi1, pj1, gc, gd;
+    tri(lane, pi0, pj0);
+    tri(lane + 64 < 78 ? lane + 64 : 0, pi1, pj1);
+    tri(lane < 21 ? lane : 0, gc, gd);
+    const bool p1 = lane + 64 < 78;
+    // column j of A: extra rows ar1, ar2 with coefficients dt * (x1 + y1 cos
+    // + z1 sin), dt * (y2 cos + z2 sin)
+    struct ACol {
+      int r1, r2;
+      double x1, y1, z1, y2, z2;
+    };
+    auto acol = [&](int j) -> ACol {
+      ACol c{j, j, 0.0, 0.0, 0.0, 0.0, 0.0};
+      if (j >= 6 && j < 9) { c.r1 = j - 6; c.x1 = dt; }
+      else if (j == 9) { c.r1 = 3; c.r2 = 4; c.y1 = dt; c.z2 = -dt; }
+      else if (j == 10) { c.r1 = 3; c.r2 = 4; c.z1 = dt; c.y2 = dt; }
+      else if (j == 11) { c.r1 = 5; c.x1 = dt; }
+      return c;
+    };
     wsync();
     double nbad = 0.0;
     for (int k = N - 1; k >= 0; --k) {
       const double cp = cs[2 * k], sp = cs[2 * k + 1];
       const bool stance = cc[k] != 0.0;
       const double* bwk = bw + 18 * k;
-      // B[r][c] (rows 6..11), zero columns for fixed variables
-      auto bent = [&](int r, int c) -> double {
-        const bool fr = c >= 3 || (stance && !(VAR == 2 && c == 1));
-        if (!fr) return 0.0;
-        if (r < 9) return c < 3 ? bv<VAR>(r - 6, c, dtm, cp, sp) : 0.0;
-        return bwk[6 * (r - 9) + c];
-      };
+      auto freec = [&](int c) { return c >= 3 || (stance && !(VAR == 2 && c == 1)); };
+      // B[6 + r][c], r < 3 (the force map; 3f: dtm I, 2f: dtm Rz')
+      auto bforce = [&](int r, int c) -> double { return c < 3 ? bv<VAR>(r, c, dtm, cp, sp) : 0.0; };
       RS_T(t_fa);
-      // (a) T = P B and M1 = P A (both read P only)
-      for (int e = lane; e < 216; e += RT) {
-        if (e < 72) {
+      // (a) T[i][c] = sum_r P[i][6 + r] B[6 + r][c] + P[i][9 + r] BW[r][c]
+      {
+        auto titem = [&](int e) -> double {
           const int i = e / 6, c = e - 6 * i;
-          double acc = 0.0;
-#pragma unroll
-          for (int r = 6; r < 12; ++r) acc = fma(P[12 * i + r], bent(r, c), acc);
-          T[e] = acc;
-        } else {
-          const int e2 = e - 72, i = e2 / 12, j = e2 - 12 * i;
-          double m1 = P[e2];
-          if (j >= 6 && j < 9) m1 = fma(dt, P[12 * i + j - 6], m1);
-          else if (j == 9) m1 += dt * (cp * P[12 * i + 3] - sp * P[12 * i + 4]);
-          else if (j == 10) m1 += dt * (sp * P[12 * i + 3] + cp * P[12 * i + 4]);
-          else if (j == 11) m1 = fma(dt, P[12 * i + 5], m1);
-          M1[e2] = m1;
-        }
+          const double* pr = Pc + 12 * i;
+          double acc = pr[9] * bwk[c];
+          acc = fma(pr[10], bwk[6 + c], acc);
+          acc = fma(pr[11], bwk[12 + c], acc);
+          if (c < 3) {
+            acc = fma(pr[6], bforce(0, c), acc);
+            acc = fma(pr[7], bforce(1, c), acc);
+            acc = fma(pr[8], bforce(2, c), acc);
+          }
+          return freec(c) ? acc : 0.0;
+        };
+        const double t0 = titem(lane);
+        const double t1 = titem(lane < 8 ? lane + 64 : 0);
+        T[lane] = t0;
+        if (lane < 8) T[lane + 64] = t1;
       }
       wsync();
       RS_ACC(11, t_fa);
       RS_T(t_fb);
-      // (b) G = 2V + B'T (identity rows for fixed variables), F = T'A
-      for (int e = lane; e < 108; e += RT) {
-        if (e < 36) {
-          const int c = e / 6, d = e - 6 * c;
-          double acc = 0.0;
-#pragma unroll
-          for (int r = 6; r < 12; ++r) acc = fma(bent(r, c), T[6 * r + d], acc);
-          const bool frc = c >= 3 || (stance && !(VAR == 2 && c == 1));
-          if (c == d) acc = frc ? acc + ((k < N - 1) ? 2.0 * kRdiag : 0.0) : 1.0;
-          G[e] = acc;
-        } else {
+      // (b) G = 2V + B'T (identity for fixed), F[c][j] = (T'A)[c][j]
+      {
+        auto gfitem = [&](int e) -> double {
+          if (e < 36) {
+            const int c = e / 6, d = e - 6 * c;
+            double acc = bwk[c] * T[54 + d];
+            acc = fma(bwk[6 + c], T[60 + d], acc);
+            acc = fma(bwk[12 + c], T[66 + d], acc);
+            if (c < 3) {
+              acc = fma(bforce(0, c), T[36 + d], acc);
+              acc = fma(bforce(1, c), T[42 + d], acc);
+              acc = fma(bforce(2, c), T[48 + d], acc);
+            }
+            if (!freec(c)) return c == d ? 1.0 : 0.0;
+            return c == d ? acc + ((k < N - 1) ? 2.0 * kRdiag : 0.0) : acc;
+          }
           const int e2 = e - 36, c = e2 / 12, j = e2 - 12 * c;
+          const ACol aj = acol(j);
           double f = T[6 * j + c];
-          if (j >= 6 && j < 9) f = fma(dt, T[6 * (j - 6) + c], f);
-          else if (j == 9) f += dt * (cp * T[18 + c] - sp * T[24 + c]);
-          else if (j == 10) f += dt * (sp * T[18 + c] + cp * T[24 + c]);
-          else if (j == 11) f = fma(dt, T[30 + c], f);
-          F[e2] = f;
-        }
+          f = fma(aj.x1 + aj.y1 * cp + aj.z1 * sp, T[6 * aj.r1 + c], f);
+          f = fma(aj.y2 * cp + aj.z2 * sp, T[6 * aj.r2 + c], f);
+          return f;
+        };
+        const double g0 = gfitem(lane);
+        const double g1 = gfitem(lane < 44 ? lane + 64 : 0);
+        if (lane < 36) G[lane] = g0;
+        else F[lane - 36] = g0;
+        if (lane < 44) F[lane + 28] = g1;
       }
       wsync();
       RS_ACC(12, t_fb);
@@ -352,11 +407,11 @@ __device__ void ric_solve(const SolveArgs& a, const int N, const int64_t b, doub
           Di[loff(r) + c] = -s * dinv[r];
         }
       }
-      double* Dl = un + DL_OFF;   // Dinv, packed lower
-      double* Kl = un + KL_OFF;   // K_k (the P update reads it)
-      if (lane == 0) {
+      if (lane < 21) {   // Dinv entry (gc, gd) -- a lane-constant index
+        double v = 0.0;
 #pragma unroll
-        for (int e = 0; e < 21; ++e) Dl[e] = Di[e];
+        for (int e = 0; e < 21; ++e) v = (e == lane) ? Di[e] : v;
+        Dl[lane] = v;
       }
       if (lane < 12) {
         const int j = lane;
@@ -380,33 +435,44 @@ __device__ void ric_solve(const SolveArgs& a, const int N, const int64_t b, doub
       wsync();
       RS_ACC(13, t_fc);
       RS_T(t_fd);
-      // (d) G^-1 = Dinv'Dinv (lanes < 21) and P_k = 2Q + A'(P A) - F'K (lower
-      // triangle, mirrored)
-      if (lane < 21) {   // G^-1 (c, d), c >= d: sum_{m >= c} Dinv[m][c] Dinv[m][d]
-        int c = 0;
-        while (loff(c + 1) <= lane) ++c;
-        const int d = lane - loff(c);
+      // (d) G^-1 (gc, gd) = sum_{m >= gc} Dinv[m][gc] Dinv[m][gd] (lanes < 21);
+      // P_k (i, j), j <= i, mirrored
+      if (lane < 21) {
         double s = 0.0;
-        for (int m = c; m < 6; ++m) s = fma(Dl[loff(m) + c], Dl[loff(m) + d], s);
+#pragma unroll
+        for (int m = 0; m < 6; ++m)
+          if (m >= gc) s = fma(Dl[loff(m) + gc], Dl[loff(m) + gd], s);
         gi[21 * k + lane] = s;
       }
       if (k == 0) break;
-      for (int e = lane; e < 78; e += RT) {
-        int i = 0;
-        while (loff(i + 1) <= e) ++i;
-        const int j = e - loff(i);
-        double pn = M1[12 * i + j];
-        if (i >= 6 && i < 9) pn = fma(dt, M1[12 * (i - 6) + j], pn);
-        else if (i == 9) pn += dt * (cp * M1[36 + j] - sp * M1[48 + j]);
-        else if (i == 10) pn += dt * (sp * M1[36 + j] + cp * M1[48 + j]);
-        else if (i == 11) pn = fma(dt, M1[60 + j], pn);
+      {
+        auto pitem = [&](int i, int j) -> double {
+          const ACol ai = acol(i), aj = acol(j);
+          const double q = (i == j) ? 2.0 * qdiag(i) : 0.0;
+          const double ca1 = ai.x1 + ai.y1 * cp + ai.z1 * sp, ca2 = ai.y2 * cp + ai.z2 * sp;
+          const double cb1 = aj.x1 + aj.y1 * cp + aj.z1 * sp, cb2 = aj.y2 * cp + aj.z2 * sp;
+          const double* r0 = Pc + 12 * i;
+          const double* r1 = Pc + 12 * ai.r1;
+          const double* r2 = Pc + 12 * ai.r2;
+          const double s0 = fma(cb2, r0[aj.r2], fma(cb1, r0[aj.r1], r0[j]));
+          const double s1 = fma(cb2, r1[aj.r2], fma(cb1, r1[aj.r1], r1[j]));
+          const double s2 = fma(cb2, r2[aj.r2], fma(cb1, r2[aj.r1], r2[j]));
+          double pn = fma(ca2, s2, fma(ca1, s1, s0)) + q;
 #pragma unroll
-        for (int c = 0; c < 6; ++c) pn = fma(-F[12 * c + i], Kl[12 * c + j], pn);
-        if (i == j) pn += 2.0 * kQ[i];
-        P[12 * i + j] = pn;
-        P[12 * j + i] = pn;
+          for (int c = 0; c < 6; ++c) pn = fma(-F[12 * c + i], Kl[12 * c + j], pn);
+          return pn;
+        };
+        const double v0 = pitem(pi0, pj0);
+        Pn[12 * pi0 + pj0] = v0;
+        Pn[12 * pj0 + pi0] = v0;
+        if (p1) {
+          const double v1 = pitem(pi1, pj1);
+          Pn[12 * pi1 + pj1] = v1;
+          Pn[12 * pj1 + pi1] = v1;
+        }
       }
       wsync();
+      double* tmp = Pc; Pc = Pn; Pn = tmp;
       RS_ACC(14, t_fd);
     }
     if (nbad != 0.0) status = ST_NUMERICAL;
@@ -424,71 +490,72 @@ __device__ void ric_solve(const SolveArgs& a, const int N, const int64_t b, doub
   //             x_{k+1}[i] = (A_k x)[i] + B_k[i,:] u_k    (lane i < 12)
   // Every step's data (K_k from the global workspace, B_k / w_k from LDS) is
   // loaded two steps ahead (a three-deep register ring).
-  // per-lane constants of the A maps (see the shift comments below)
-  const double gA = (lane >= 6 && lane <= 8) || lane == 11 ? dt : 0.0;   // bwd s6, fixed
-  const double gB = (lane == 9 || lane == 10) ? dt : 0.0;                // bwd s6, * cos
-  const double gC = lane == 9 ? -dt : 0.0;                               // bwd s5, * sin
-  const double gD = lane == 10 ? dt : 0.0;                               // bwd s7, * sin
-  const double fA = lane < 3 || lane == 5 ? dt : 0.0;                    // fwd s6, fixed
-  const double fB = (lane == 3 || lane == 4) ? dt : 0.0;                 // fwd s6, * cos
-  const double fC = lane == 3 ? dt : 0.0;                                // fwd s7, * sin
-  const double fD = lane == 4 ? -dt : 0.0;                               // fwd s5, * sin
-  const int c6 = lane < 6 ? lane : 0;
-  // force map rows 6..8 of B_k = dtm (3f: I; 2f: Rz(psi)') as per-lane
-  // coefficients P + Q cos + S sin, branch-free:
-  //   k*[r] (backward, lane c < 6):  B[6+r][c]
-  //   r*[c] (forward, lane 6+r):     B[6+r][c]
-  double kP[3], kQ_[3], kS[3], rP[3], rQ[3], rS[3];
-#pragma unroll
-  for (int r = 0; r < 3; ++r) {
-    const double on_b = lane == r ? dtm : 0.0, on_f = lane == 6 + r ? dtm : 0.0;
-    if constexpr (VAR == 3) {
-      kP[r] = on_b; kQ_[r] = 0.0; kS[r] = 0.0;
-      rP[r] = on_f; rQ[r] = 0.0; rS[r] = 0.0;
-    } else {   // Rz' = [[c, -s, 0], [s, c, 0], [0, 0, 1]]
-      kP[r] = r == 2 ? on_b : 0.0;
-      kQ_[r] = r < 2 ? on_b : 0.0;
-      kS[r] = r == 0 ? (lane == 1 ? -dtm : 0.0) : (r == 1 ? (lane == 0 ? dtm : 0.0) : 0.0);
-      rP[r] = r == 2 ? (lane == 8 ? dtm : 0.0) : 0.0;
-      rQ[r] = r < 2 ? on_f : 0.0;   // column r of row r: cos
-      rS[r] = r == 0 ? (lane == 7 ? dtm : 0.0) : (r == 1 ? (lane == 6 ? -dtm : 0.0) : 0.0);
-    }
-  }
-  const double m911 = (lane >= 9 && lane < 12) ? 1.0 : 0.0;
   struct BwdL {
     double cp, sp, st, b0, b1, b2, n, kc[6];
   };
   struct FwdL {
     double cp, sp, w, kr[12], br[6];
   };
-  auto load_b = [&](int j, BwdL& d) __attribute__((always_inline)) {
-    d.cp = cs[2 * j];
-    d.sp = cs[2 * j + 1];
-    d.st = cc[j];
-    d.b0 = bw[18 * j + c6];
-    d.b1 = bw[18 * j + 6 + c6];
-    d.b2 = bw[18 * j + 12 + c6];
-    d.n = nb[6 * j + c6];
-    const double* kcol = km + 72 * j + (lane < 12 ? lane : 0);
-#pragma unroll
-    for (int c = 0; c < 6; ++c) d.kc[c] = kcol[12 * c];
-    asm volatile("" ::: "memory");   // issue here, two steps ahead of the use
-  };
-  auto load_f = [&](int k, FwdL& d) __attribute__((always_inline)) {
-    d.cp = cs[2 * k];
-    d.sp = cs[2 * k + 1];
-    d.w = mu_[6 * k + c6];
-    const double* krow = km + 72 * k + 12 * c6;
-#pragma unroll
-    for (int c = 0; c < 12; ++c) d.kr[c] = krow[c];
-    const int rr = (lane >= 9 && lane < 12) ? lane - 9 : 0;
-#pragma unroll
-    for (int c = 0; c < 6; ++c) d.br[c] = bw[18 * k + 6 * rr + c];
-    asm volatile("" ::: "memory");   // issue here, two steps ahead of the use
-  };
   // jt (uniform): the last stage where the right-hand side NB is nonzero --
   // the backward sweep starts there (lam_{jt+1} = 0, mu_j = 0 beyond it)
   auto hinv = [&](double* dst, int jt) __attribute__((always_inline)) {
+    // (lane constants made here, per call: not live across the active set)
+    // per-lane constants of the A maps (see the shift comments below)
+    const double gA = (lane >= 6 && lane <= 8) || lane == 11 ? dt : 0.0;   // bwd s6, fixed
+    const double gB = (lane == 9 || lane == 10) ? dt : 0.0;                // bwd s6, * cos
+    const double gC = lane == 9 ? -dt : 0.0;                               // bwd s5, * sin
+    const double gD = lane == 10 ? dt : 0.0;                               // bwd s7, * sin
+    const double fA = lane < 3 || lane == 5 ? dt : 0.0;                    // fwd s6, fixed
+    const double fB = (lane == 3 || lane == 4) ? dt : 0.0;                 // fwd s6, * cos
+    const double fC = lane == 3 ? dt : 0.0;                                // fwd s7, * sin
+    const double fD = lane == 4 ? -dt : 0.0;                               // fwd s5, * sin
+    const int c6 = lane < 6 ? lane : 0;
+    // force map rows 6..8 of B_k = dtm (3f: I; 2f: Rz(psi)') as per-lane
+    // coefficients P + Q cos + S sin, branch-free:
+    //   k*[r] (backward, lane c < 6):  B[6+r][c]
+    //   r*[c] (forward, lane 6+r):     B[6+r][c]
+    double kP[3], kQ_[3], kS[3], rP[3], rQ[3], rS[3];
+  #pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      const double on_b = lane == r ? dtm : 0.0, on_f = lane == 6 + r ? dtm : 0.0;
+      if constexpr (VAR == 3) {
+        kP[r] = on_b; kQ_[r] = 0.0; kS[r] = 0.0;
+        rP[r] = on_f; rQ[r] = 0.0; rS[r] = 0.0;
+      } else {   // Rz' = [[c, -s, 0], [s, c, 0], [0, 0, 1]]
+        kP[r] = r == 2 ? on_b : 0.0;
+        kQ_[r] = r < 2 ? on_b : 0.0;
+        kS[r] = r == 0 ? (lane == 1 ? -dtm : 0.0) : (r == 1 ? (lane == 0 ? dtm : 0.0) : 0.0);
+        rP[r] = r == 2 ? (lane == 8 ? dtm : 0.0) : 0.0;
+        rQ[r] = r < 2 ? on_f : 0.0;   // column r of row r: cos
+        rS[r] = r == 0 ? (lane == 7 ? dtm : 0.0) : (r == 1 ? (lane == 6 ? -dtm : 0.0) : 0.0);
+      }
+    }
+    const double m911 = (lane >= 9 && lane < 12) ? 1.0 : 0.0;
+    auto load_b = [&](int j, BwdL& d) __attribute__((always_inline)) {
+      d.cp = cs[2 * j];
+      d.sp = cs[2 * j + 1];
+      d.st = cc[j];
+      d.b0 = bw[18 * j + c6];
+      d.b1 = bw[18 * j + 6 + c6];
+      d.b2 = bw[18 * j + 12 + c6];
+      d.n = nb[6 * j + c6];
+      const double* kcol = km + 72 * j + (lane < 12 ? lane : 0);
+  #pragma unroll
+      for (int c = 0; c < 6; ++c) d.kc[c] = kcol[12 * c];
+      asm volatile("" ::: "memory");   // issue here, two steps ahead of the use
+    };
+    auto load_f = [&](int k, FwdL& d) __attribute__((always_inline)) {
+      d.cp = cs[2 * k];
+      d.sp = cs[2 * k + 1];
+      d.w = mu_[6 * k + c6];
+      const double* krow = km + 72 * k + 12 * c6;
+  #pragma unroll
+      for (int c = 0; c < 12; ++c) d.kr[c] = krow[c];
+      const int rr = (lane >= 9 && lane < 12) ? lane - 9 : 0;
+  #pragma unroll
+      for (int c = 0; c < 6; ++c) d.br[c] = bw[18 * k + 6 * rr + c];
+      asm volatile("" ::: "memory");   // issue here, two steps ahead of the use
+    };
     // ---- backward sweep
     {
       double li = 0.0;                                  // lam_{j+1}[lane]
@@ -970,7 +1037,11 @@ __device__ void ric_solve(const SolveArgs& a, const int N, const int64_t b, doub
     }
     return;
   }
-  // x* staged over SV.. (x_ref read from global in the objective)
+  // x_ref into the union again (over the dead R), x* staged over SV..
+  for (int i = lane; i < 12 * N; i += RT) {
+    const int r = i / 12, c = i - 12 * r;
+    un[i] = xrf[(int64_t)r * a.xref_rs + c];
+  }
   for (int i = lane; i < NV; i += RT) {
     const int j = i / 6, c = i - 6 * j;
     const bool fr = c >= 3 || (cc[j] != 0.0 && !(VAR == 2 && c == 1));
@@ -1000,7 +1071,7 @@ __device__ void ric_solve(const SolveArgs& a, const int N, const int64_t b, doub
       }
       xr = lane < 12 ? nx : 0.0;
       const double kf = (k == N - 1) ? kTermQ : 1.0;
-      const double e = lane < 12 ? xr - xrf[(int64_t)k * a.xref_rs + lane] : 0.0;
+      const double e = lane < 12 ? xr - un[12 * k + lane] : 0.0;
       objl = fma(kf * qr * e, e, objl);
       if (k < N - 1 && lane < 6) {
         const double ub = a.uref_aliased ? ub_alias : ((cc[k] != 0.0) ? 2.0 * a.m * a.g : 0.0);
