@@ -71,7 +71,7 @@ def workload_label(args, world):
     reference's own CPU run.py, whose MPC horizon is N = 60)."""
     gb = args.global_batch or args.batch * world
     curve = not args.straight
-    if args.precision == 'f32' and args.variant == '3f' and args.N == 10:
+    if args.precision in ('f32', 'f32_generic') and args.variant == '3f' and args.N == 10:
         return f'configs[4]: batch={gb}, 3f, N=10, fp32 (vs fp64) tolerance/throughput trade-off'
     if args.variant == '2f' and args.N == 10 and not curve:
         return f'configs[1]: batch={gb} randomised x0, 2f (planar, Fy=0), horizon N=10, fp64'
@@ -101,7 +101,7 @@ def parse():
     ap.add_argument('--mu-sweep', action='store_true', help='mu ~ U(0.3, 1.2)')
     ap.add_argument('--seed', type=int, default=2024)
     ap.add_argument('--precision', default='f64',
-                    choices=['f64', 'f32', 'f64_generic', 'f64_riccati', 'f64_dense'],
+                    choices=['f64', 'f32', 'f64_generic', 'f64_riccati', 'f64_dense', 'f32_generic'],
                     help='f64 = the fastest fp64 kernel for N (default); f32 = fp32 one-wave '
                          'kernel (configs[4]); others force a kernel for A/B runs')
     ap.add_argument('--cpu-seconds', type=float, default=12.0,
@@ -316,7 +316,7 @@ def main():
             'higher_is_better': True,
             'scaling': 'strong' if args.global_batch else 'weak',
             'vs_baseline': None,
-            'dtype': 'f32' if args.precision == 'f32' else 'f64',
+            'dtype': 'f32' if args.precision in ('f32', 'f32_generic') else 'f64',
             'data': 'synthetic: Runner path_plan_init plan + randomised x0 (SURVEY.md 8d), generated on '
                     'host, resident in HBM before timing',
             'config': {'workload': workload_label(args, world), 'global_batch': B * world

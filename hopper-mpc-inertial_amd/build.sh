@@ -7,6 +7,8 @@ set -euo pipefail
 cd "$(dirname "$0")"
 HIPCC=${HIPCC:-/opt/rocm/bin/hipcc}
 HORIZONS=${HORIZONS:-"5 10 20"}
+F32_HORIZONS=${F32_HORIZONS:-"10"}   # fp32 builds of the dense kernel (BASELINE configs[4])
+F32_WAVES=${F32_WAVES:-3}           # their waves / SIMD (3: <= 168 VGPRs, no spill)
 JOBS=${JOBS:-8}
 OUT=${OUT:-libhmpc.so}
 BDIR=${BDIR:-build}
@@ -14,13 +16,21 @@ FLAGS="--offload-arch=gfx950 -O3 -fPIC -std=c++17 -Wno-unused-result"
 mkdir -p $BDIR
 LIST=""
 for n in $HORIZONS; do LIST="$LIST X($n)"; done
+F32LIST=""
+for n in $F32_HORIZONS; do F32LIST="$F32LIST X($n)"; done
 pids=()
 for n in $HORIZONS; do
   $HIPCC $FLAGS -DHMPC_INST_N=$n -c csrc/hmpc_kernels.hip -o $BDIR/hmpc_kernels_n$n.o "$@" &
   pids+=($!)
   while [ "$(jobs -rp | wc -l)" -ge "$JOBS" ]; do sleep 1; done
 done
-$HIPCC $FLAGS "-DHMPC_HORIZON_LIST(X)=$LIST" -c csrc/hmpc_dispatch.cpp -o $BDIR/hmpc_dispatch.o &
+for n in $F32_HORIZONS; do
+  # fp32: 3 waves / SIMD fit (<= 168 VGPRs, 9.9 KB LDS) without spilling
+  $HIPCC $FLAGS -DHMPC_INST_N=$n -DHMPC_REAL=float -DHMPC_LAUNCH_SUFFIX=_f32 "-DHMPC_WAVES_PER_EU(W)=$F32_WAVES" \
+    -c csrc/hmpc_kernels.hip -o $BDIR/hmpc_kernels_n${n}_f32.o "$@" &
+  pids+=($!)
+done
+$HIPCC $FLAGS "-DHMPC_HORIZON_LIST(X)=$LIST" "-DHMPC_F32_LIST(X)=$F32LIST" -c csrc/hmpc_dispatch.cpp -o $BDIR/hmpc_dispatch.o &
 pids+=($!)
 $HIPCC $FLAGS -c csrc/hmpc_capi.cpp -o $BDIR/hmpc_capi.o &
 pids+=($!)
@@ -33,6 +43,7 @@ pids+=($!)
 for p in "${pids[@]}"; do wait "$p"; done
 objs=""
 for n in $HORIZONS; do objs="$objs $BDIR/hmpc_kernels_n$n.o"; done
+for n in $F32_HORIZONS; do objs="$objs $BDIR/hmpc_kernels_n${n}_f32.o"; done
 $HIPCC --offload-arch=gfx950 -shared -fPIC $objs $BDIR/hmpc_dispatch.o $BDIR/hmpc_capi.o $BDIR/hmpc_plant.o $BDIR/hmpc_wide.o $BDIR/hmpc_ric.o -o $OUT.tmp
 mv $OUT.tmp $OUT
 echo "built $(pwd)/$OUT (horizons: $HORIZONS)"

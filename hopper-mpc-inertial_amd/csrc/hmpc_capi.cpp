@@ -123,7 +123,10 @@ int prepare_ric(hmpc_ctx* c, int64_t B, hmpc::SolveArgs& a) {
   const hmpc::Kernel k = hmpc::pick_kernel(c->variant, c->N, c->precision);
   a.ovf_count = nullptr; a.ovf_list = nullptr; a.rws = nullptr; a.rws_stride = 0;
   a.work = nullptr; a.kws = nullptr; a.kws_stride = 0; a.ric_groups = 0;
-  if ((k != hmpc::Kernel::Dense && k != hmpc::Kernel::Riccati) || c->N > hmpc::kRicNmax) return HMPC_OK;
+  // (the fp32 dense build hands its overflows to the same fp64 pass)
+  if ((k != hmpc::Kernel::Dense && k != hmpc::Kernel::DenseF32 && k != hmpc::Kernel::Riccati) ||
+      c->N > hmpc::kRicNmax)
+    return HMPC_OK;
   const int64_t rstride = hmpc::ric_rws_stride(c->N);
   if (!c->rws) {
     hipError_t e = hipMalloc(&c->rws, sizeof(double) * rstride * kOvfGroups);
@@ -253,7 +256,8 @@ const char* hmpc_last_error(hmpc_ctx* c) { return c ? c->err.c_str() : ""; }
 int hmpc_active_capacity(hmpc_ctx* c) {
   if (!c) return -1;
   switch (hmpc::pick_kernel(c->variant, c->N, c->precision)) {
-    case hmpc::Kernel::Dense: {
+    case hmpc::Kernel::Dense:
+    case hmpc::Kernel::DenseF32: {
       const int nv = 6 * c->N, q = c->N <= 10 ? 20 : 48;
       return nv < 20 ? nv : q;   // QMAX of hmpc_kernels.hip
     }
@@ -272,16 +276,19 @@ const char* hmpc_kernel_name(hmpc_ctx* c) {
   switch (hmpc::pick_kernel(c->variant, c->N, c->precision)) {
     case hmpc::Kernel::Dense: {
       static const char* names[2][3] = {
-          {"hmpc::solve_kernel<2, 5>", "hmpc::solve_kernel<2, 10>", "hmpc::solve_kernel<2, 20>"},
-          {"hmpc::solve_kernel<3, 5>", "hmpc::solve_kernel<3, 10>", "hmpc::solve_kernel<3, 20>"}};
+          {"hmpc::solve_kernel<2, 5, double>", "hmpc::solve_kernel<2, 10, double>", "hmpc::solve_kernel<2, 20, double>"},
+          {"hmpc::solve_kernel<3, 5, double>", "hmpc::solve_kernel<3, 10, double>", "hmpc::solve_kernel<3, 20, double>"}};
       const int i = c->N == 5 ? 0 : (c->N == 10 ? 1 : 2);
       return names[v3][i];
     }
+    case hmpc::Kernel::DenseF32:
+      return v3 ? "hmpc::solve_kernel<3, 10, float>" : "hmpc::solve_kernel<2, 10, float>";
     case hmpc::Kernel::Riccati:
       if (hmpc::ric_occ(c->N) == 2) return v3 ? "hmpc::ric_kernel<3, 2>" : "hmpc::ric_kernel<2, 2>";
       return v3 ? "hmpc::ric_kernel<3, 1>" : "hmpc::ric_kernel<2, 1>";
     case hmpc::Kernel::Wide:
-      if (c->precision == HMPC_PREC_F32) return v3 ? "hmpc::wide_kernel<3, float>" : "hmpc::wide_kernel<2, float>";
+      if (c->precision == HMPC_PREC_F32 || c->precision == HMPC_PREC_F32_GENERIC)
+        return v3 ? "hmpc::wide_kernel<3, float>" : "hmpc::wide_kernel<2, float>";
       return v3 ? "hmpc::wide_kernel<3, double>" : "hmpc::wide_kernel<2, double>";
     default:
       return "";
@@ -291,7 +298,8 @@ const char* hmpc_kernel_name(hmpc_ctx* c) {
 int hmpc_set_precision(hmpc_ctx* c, int precision) {
   if (!c) return HMPC_ERR_ARG;
   if (precision != HMPC_PREC_F64 && precision != HMPC_PREC_F32 && precision != HMPC_PREC_F64_GENERIC &&
-      precision != HMPC_PREC_F64_RICCATI && precision != HMPC_PREC_F64_DENSE) {
+      precision != HMPC_PREC_F64_RICCATI && precision != HMPC_PREC_F64_DENSE &&
+      precision != HMPC_PREC_F32_GENERIC) {
     c->err = "unknown precision";
     return HMPC_ERR_ARG;
   }

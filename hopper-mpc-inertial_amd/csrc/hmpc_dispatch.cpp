@@ -9,12 +9,28 @@
 #ifndef HMPC_HORIZON_LIST
 #define HMPC_HORIZON_LIST(X) X(5) X(10) X(20)
 #endif
+// horizons with an fp32 build of the dense kernel (launch_solve_n<N>_f32)
+#ifndef HMPC_F32_LIST
+#define HMPC_F32_LIST(X) X(10)
+#endif
 
 namespace hmpc {
 
 #define HMPC_DECL(n) bool launch_solve_n##n(int variant, const SolveArgs& a, hipStream_t s);
 HMPC_HORIZON_LIST(HMPC_DECL)
 #undef HMPC_DECL
+#define HMPC_DECL(n) bool launch_solve_n##n##_f32(int variant, const SolveArgs& a, hipStream_t s);
+HMPC_F32_LIST(HMPC_DECL)
+#undef HMPC_DECL
+
+static bool f32_compiled(int variant, int N) {
+  if (variant != 2 && variant != 3) return false;
+#define HMPC_CASE(n) \
+  if (N == n) return true;
+  HMPC_F32_LIST(HMPC_CASE)
+#undef HMPC_CASE
+  return false;
+}
 
 bool horizon_compiled(int variant, int N) {
   if (variant != 2 && variant != 3) return false;
@@ -29,7 +45,10 @@ Kernel pick_kernel(int variant, int N, int precision) {
   if (variant != 2 && variant != 3 || N < 1) return Kernel::None;
   switch (precision) {
     case 1:
+      if (f32_compiled(variant, N)) return Kernel::DenseF32;
+      return N <= kWideNmax ? Kernel::Wide : Kernel::None;
     case 2:
+    case 5:
       return N <= kWideNmax ? Kernel::Wide : Kernel::None;
     case 3:
       return N <= kRicNmax ? Kernel::Riccati : Kernel::None;
@@ -53,6 +72,12 @@ bool launch_solve(int variant, int N, const SolveArgs& a, hipStream_t s) {
 #define HMPC_CASE(n) \
   if (N == n) return launch_solve_n##n(variant, a, s);
       HMPC_HORIZON_LIST(HMPC_CASE)
+#undef HMPC_CASE
+      return false;
+    case Kernel::DenseF32:
+#define HMPC_CASE(n) \
+  if (N == n) return launch_solve_n##n##_f32(variant, a, s);
+      HMPC_F32_LIST(HMPC_CASE)
 #undef HMPC_CASE
       return false;
     case Kernel::Riccati:

@@ -146,7 +146,7 @@ void launch_plant(const PlantArgs& a, hipStream_t s);
 void launch_convert(int64_t B, const double* X, double* x, hipStream_t s);
 
 // Which kernel solves (variant, N) at a precision (HMPC_PREC_*).
-enum class Kernel { None, Dense, Riccati, Wide };
+enum class Kernel { None, Dense, DenseF32, Riccati, Wide };
 Kernel pick_kernel(int variant, int N, int precision);
 // Launch the solve kernel for (variant, N, a.precision).  Returns false when
 // no kernel serves that combination.  Dense and Riccati kernels honour

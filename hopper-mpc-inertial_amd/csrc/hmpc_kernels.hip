@@ -1,4 +1,5 @@
-// hmpc_kernels.hip -- batched MPC/QP solve for MI355X (gfx950), fp64.
+// hmpc_kernels.hip -- batched MPC/QP solve for MI355X (gfx950), fp64 (and
+// an fp32 build of the same kernel for BASELINE configs[4]).
 //
 // One workgroup of W = ceil(6N/64) wavefronts solves ONE QP instance of the
 // reference's Mpc.build_qp/solve_qp (src/mpc_cvx_euler_3f.py:96-160; 2f
@@ -38,6 +39,12 @@
 //      its constant term evaluated on (x*, u*), status, iterations.
 //
 // No MFMA: every product is a tiny dense block or a rank-1 update.
+//
+// The arithmetic type `real` is fixed per object: double (the product path,
+// launch_solve_n<N>) or, built with -DHMPC_REAL=float, float
+// (launch_solve_n<N>_f32: inputs and outputs stay fp64 in HBM, every
+// operation in between is fp32).  Everything but the launcher sits in an
+// anonymous namespace, so the two builds never share a symbol.
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
@@ -47,7 +54,22 @@
 #include "hmpc_internal.h"
 #include "hmpc_model.h"
 
+#ifndef HMPC_REAL
+#define HMPC_REAL double
+#endif
+
 namespace hmpc {
+namespace {
+
+using real = HMPC_REAL;
+constexpr bool kF32 = sizeof(real) == 4;
+// feasibility tolerance of the slack scan and the relative threshold on
+// |w_perp|^2 for a usable primal direction, per precision
+constexpr real kTolR = kF32 ? real(2e-4) : real(kTol);
+constexpr real kZnRel = kF32 ? real(1e-10) : real(1e-24);
+
+__device__ __forceinline__ void sincos_r(double x, double* s, double* c) { sincos(x, s, c); }
+__device__ __forceinline__ void sincos_r(float x, float* s, float* c) { sincosf(x, s, c); }
 
 // compile-time loop: f(std::integral_constant<int, i>) for i in [Begin, End).
 // Every index into a register-resident row goes through this (or the ladders
@@ -82,8 +104,8 @@ __device__ __forceinline__ void at_index(int n, F&& f) {
 
 // Empty asm that claims to read and write x: pins the value into a VGPR pair
 // at this point, so the scheduler cannot sink a step's FMAs past the next
-// step's loads (which would double the live set and spill the row).
-__device__ __forceinline__ void pin(double& x) { asm volatile("" : "+v"(x)); }
+// step's loads (which would real the live set and spill the row).
+__device__ __forceinline__ void pin(real& x) { asm volatile("" : "+v"(x)); }
 // A wave-uniform 0 the compiler cannot see through.  Added to an LDS address
 // it keeps the loads behind it from being hoisted above this point (the
 // scheduler otherwise pulls every load of a long unrolled loop to the top
@@ -99,31 +121,35 @@ __device__ __forceinline__ int opaque_zero() {
 // the value is valid only after the matching lds_wait (s_waitcnt lgkmcnt(n),
 // n = LDS instructions issued after the load), which also ties the registers
 // so nothing reads them earlier.
-typedef double dbl2 __attribute__((ext_vector_type(2)));
+typedef real real2 __attribute__((ext_vector_type(2)));
+constexpr int RB = (int)sizeof(real);   // bytes per element
 __device__ __forceinline__ unsigned lds_addr(const void* p) {
   return (unsigned)(uintptr_t)p;   // low 32 bits of the flat address = LDS offset
 }
+// two consecutive elements (OFF in bytes); one element
 template <int OFF>
-__device__ __forceinline__ void lds_ld128(dbl2& v, unsigned base) {
-  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(base), "i"(OFF) : "memory");
+__device__ __forceinline__ void lds_ld2(real2& v, unsigned base) {
+  if constexpr (kF32) asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(v) : "v"(base), "i"(OFF) : "memory");
+  else asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(base), "i"(OFF) : "memory");
 }
-__device__ __forceinline__ void lds_ld64(double& v, unsigned addr) {
-  asm volatile("ds_read_b64 %0, %1" : "=v"(v) : "v"(addr) : "memory");
+__device__ __forceinline__ void lds_ld1(real& v, unsigned addr) {
+  if constexpr (kF32) asm volatile("ds_read_b32 %0, %1" : "=v"(v) : "v"(addr) : "memory");
+  else asm volatile("ds_read_b64 %0, %1" : "=v"(v) : "v"(addr) : "memory");
 }
 template <int CNT>
-__device__ __forceinline__ void lds_wait(dbl2& a, dbl2& b, dbl2& c, dbl2& d) {
+__device__ __forceinline__ void lds_wait(real2& a, real2& b, real2& c, real2& d) {
   asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(a), "+v"(b), "+v"(c), "+v"(d) : "i"(CNT));
 }
 template <int CNT>
-__device__ __forceinline__ void lds_wait(dbl2& a, dbl2& b) {
+__device__ __forceinline__ void lds_wait(real2& a, real2& b) {
   asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(a), "+v"(b) : "i"(CNT));
 }
 template <int CNT>
-__device__ __forceinline__ void lds_wait(double& a, double& b) {
+__device__ __forceinline__ void lds_wait(real& a, real& b) {
   asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(a), "+v"(b) : "i"(CNT));
 }
 template <int CNT>
-__device__ __forceinline__ void lds_wait(double& a) {
+__device__ __forceinline__ void lds_wait(real& a) {
   asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(a) : "i"(CNT));
 }
 
@@ -137,7 +163,7 @@ struct Blk {
   }
   // `red` must hold >= 2*W doubles; calls are bracketed by barriers (W > 1)
   // so consecutive calls may reuse it.
-  __device__ __forceinline__ static double sum(double x, double* red) {
+  __device__ __forceinline__ static real sum(real x, real* red) {
     x = wave_sum(x);
     if constexpr (W == 1) {
       return x;
@@ -145,13 +171,13 @@ struct Blk {
       __syncthreads();
       if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = x;
       __syncthreads();
-      double s = 0.0;
+      real s = 0.0;
 #pragma unroll
       for (int w = 0; w < W; ++w) s += red[w];
       return s;
     }
   }
-  __device__ __forceinline__ static void argmin(double& v, int& i, double* red) {
+  __device__ __forceinline__ static void argmin(real& v, int& i, real* red) {
     wave_argmin(v, i);
     if constexpr (W > 1) {
       __syncthreads();
@@ -167,7 +193,7 @@ struct Blk {
     }
   }
   // value of x in lane l (l uniform)
-  __device__ __forceinline__ static double bcast(double x, int l, double* red) {
+  __device__ __forceinline__ static real bcast(real x, int l, real* red) {
     if constexpr (W == 1) {
       return rdlane(x, l);
     } else {
@@ -178,7 +204,7 @@ struct Blk {
     }
   }
   // first lane (over the workgroup) with flag set, or -1
-  __device__ __forceinline__ static int first(bool flag, double* red) {
+  __device__ __forceinline__ static int first(bool flag, real* red) {
     unsigned long long m = __ballot(flag);
     int f = m ? (int)__builtin_ctzll(m) + (int)(threadIdx.x & ~63u) : 0x7fffffff;
     if constexpr (W > 1) {
@@ -217,9 +243,9 @@ struct Lay {
   static constexpr int XS = ZB + e2(N + 1);        // [NT] primal broadcast
   static constexpr int RED = XS + NT;              // [4] cross-wave reductions (W <= 2)
   static constexpr int ZR = RED + 4;               // [2] a 0.0 for masked lanes' loads
-  static constexpr int XRV = ZR + 2;               // [2] x_ref view for phase 7: address, row stride
+  static constexpr int XRV = ZR + 2;               // [4] x_ref view for phase 7: address (8 B), row stride
   // active-set state (phase 6); the Cholesky's column buffers overlay it
-  static constexpr int G0 = XRV + 2;
+  static constexpr int G0 = XRV + 4;
   static constexpr int UA = G0;                    // [QMAX] active multipliers
   static constexpr int ACT = UA + QMAX;            // [QMAX] active ids (int)
   static constexpr int CB = ACT + QMAX;            // [QMAX] c = Qw' w
@@ -267,7 +293,7 @@ static_assert(kRing2 == 4 || kRing2 == 8, "ring depth");
 // ----------------------------------------------------------------------------
 // Two-wave sweeps: every wave gets all NV entries of the right-hand side
 // (rows lane and lane + 64).  `red` must hold NT doubles here (the XS row).
-__device__ __forceinline__ void sweep_stage(double b, double& a0, double& a1, double* buf) {
+__device__ __forceinline__ void sweep_stage(real b, real& a0, real& a1, real* buf) {
   const int lane = threadIdx.x & 63;
   __syncthreads();
   buf[threadIdx.x] = b;
@@ -283,8 +309,8 @@ __device__ __forceinline__ void sweep_stage(double b, double& a0, double& a1, do
 // and the sweep starts there (constraint normals are sparse: a box or
 // friction row of stage j starts at 6j).
 template <int N>
-__device__ __forceinline__ double tri_fwd_lds(double acc, const double* Mc, const double* zero,
-                                              double dinv, double* red, int s0 = 0) {
+__device__ __forceinline__ real tri_fwd_lds(real acc, const real* Mc, const real* zero,
+                                              real dinv, real* red, int s0 = 0) {
   using L = Lay<N>;
   constexpr int NV = L::NV;
   constexpr int SEND = L::W == 1 ? (NV + 3) & ~3 : ((NV + kRing2 - 1) / kRing2) * kRing2;   // padded (steps >= NV are no-ops)
@@ -293,21 +319,21 @@ __device__ __forceinline__ double tri_fwd_lds(double acc, const double* Mc, cons
     // M[tid][s] for tid > s sits at Mc[cb(s) + tid - s]; other lanes read a 0
     const unsigned base = lds_addr(Mc + tid), zaddr = lds_addr(zero);
     auto addr = [&](int s) -> unsigned {
-      return (tid > s && tid < NV && s < NV) ? base + 8u * (unsigned)(L::cb(s) - s) : zaddr;
+      return (tid > s && tid < NV && s < NV) ? base + (unsigned)RB * (unsigned)(L::cb(s) - s) : zaddr;
     };
-    double ring[4];
+    real ring[4];
     sfor<0, 4>([&](auto jc) __attribute__((always_inline)) {
-      lds_ld64(ring[decltype(jc)::value], addr(s0 + decltype(jc)::value));
+      lds_ld1(ring[decltype(jc)::value], addr(s0 + decltype(jc)::value));
     });
 #pragma unroll 1
     for (int s = s0; s < SEND; s += 4) {
       sfor<0, 4>([&](auto jc) __attribute__((always_inline)) {
         constexpr int j = decltype(jc)::value;
         const int sj = s + j;
-        const double ys = rdlane(acc, sj);
+        const real ys = rdlane(acc, sj);
         lds_wait<3>(ring[j]);
         acc = fma(-ring[j], ys, acc);
-        lds_ld64(ring[j], addr(sj + 4));
+        lds_ld1(ring[j], addr(sj + 4));
       });
     }
     lds_wait<0>(ring[0]);   // drain the ring (its last loads are dummies)
@@ -317,32 +343,32 @@ __device__ __forceinline__ double tri_fwd_lds(double acc, const double* Mc, cons
     // lane + 64) instead of exchanging one value per step through LDS and a
     // barrier; wave w keeps the rows it owns.  Loads run 4 steps ahead.
     const int lane = tid & 63;
-    double a0, a1;
+    real a0, a1;
     sweep_stage(acc, a0, a1, red);
     const unsigned b0 = lds_addr(Mc + lane), b1 = lds_addr(Mc + lane + 64), zaddr = lds_addr(zero);
     auto ad0 = [&](int s) -> unsigned {
-      return (lane > s && s < NV) ? b0 + 8u * (unsigned)(L::cb(s) - s) : zaddr;
+      return (lane > s && s < NV) ? b0 + (unsigned)RB * (unsigned)(L::cb(s) - s) : zaddr;
     };
     auto ad1 = [&](int s) -> unsigned {
-      return (lane + 64 > s && lane + 64 < NV && s < NV) ? b1 + 8u * (unsigned)(L::cb(s) - s) : zaddr;
+      return (lane + 64 > s && lane + 64 < NV && s < NV) ? b1 + (unsigned)RB * (unsigned)(L::cb(s) - s) : zaddr;
     };
     constexpr int RD = kRing2;   // s0 is a multiple of RD here
-    double r0[RD], r1[RD];
+    real r0[RD], r1[RD];
     sfor<0, RD>([&](auto jc) __attribute__((always_inline)) {
       constexpr int j = decltype(jc)::value;
-      lds_ld64(r0[j], ad0(s0 + j));
-      lds_ld64(r1[j], ad1(s0 + j));
+      lds_ld1(r0[j], ad0(s0 + j));
+      lds_ld1(r1[j], ad1(s0 + j));
     });
-    auto steps = [&](int s, const double& src, int off) __attribute__((always_inline)) {
+    auto steps = [&](int s, const real& src, int off) __attribute__((always_inline)) {
       sfor<0, RD>([&](auto jc) __attribute__((always_inline)) {
         constexpr int j = decltype(jc)::value;
         const int sj = s + j;
-        const double ys = rdlane(src, sj - off);
+        const real ys = rdlane(src, sj - off);
         lds_wait<2 * RD - 2>(r0[j], r1[j]);
         a0 = fma(-r0[j], ys, a0);
         a1 = fma(-r1[j], ys, a1);
-        lds_ld64(r0[j], ad0(sj + RD));
-        lds_ld64(r1[j], ad1(sj + RD));
+        lds_ld1(r0[j], ad0(sj + RD));
+        lds_ld1(r1[j], ad1(sj + RD));
       });
     };
 #pragma unroll 1
@@ -358,8 +384,8 @@ __device__ __forceinline__ double tri_fwd_lds(double acc, const double* Mc, cons
 // z = L^-T b (lane v holds b_v), M from the LDS copy.  One wave: loads of
 // step s-4 are issued at step s (a 4-deep ring of hand-counted loads).
 template <int N>
-__device__ __forceinline__ double tri_bwd(double acc, const double* Mc, const double* zero,
-                                          double dinv, double* red) {
+__device__ __forceinline__ real tri_bwd(real acc, const real* Mc, const real* zero,
+                                          real dinv, real* red) {
   using L = Lay<N>;
   constexpr int NV = L::NV;
   constexpr int STOP = ((NV + 3) & ~3) - 1;   // first step, padded (steps >= NV are no-ops)
@@ -370,21 +396,21 @@ __device__ __forceinline__ double tri_bwd(double acc, const double* Mc, const do
     // M[s][tid] for tid < s sits at Mc[cbt + s - tid]; other lanes read a 0
     const unsigned base = lds_addr(Mc + cbt - tid), zaddr = lds_addr(zero);
     auto addr = [&](int s) -> unsigned {
-      return (tid < s && s < NV && s >= 0) ? base + 8u * (unsigned)s : zaddr;
+      return (tid < s && s < NV && s >= 0) ? base + (unsigned)RB * (unsigned)s : zaddr;
     };
-    double ring[4];
+    real ring[4];
     sfor<0, 4>([&](auto jc) __attribute__((always_inline)) {
-      lds_ld64(ring[decltype(jc)::value], addr(STOP - decltype(jc)::value));
+      lds_ld1(ring[decltype(jc)::value], addr(STOP - decltype(jc)::value));
     });
 #pragma unroll 1
     for (int s = STOP; s >= 0; s -= 4) {
       sfor<0, 4>([&](auto jc) __attribute__((always_inline)) {
         constexpr int j = decltype(jc)::value;
         const int sj = s - j;
-        const double zs = rdlane(acc, sj);
+        const real zs = rdlane(acc, sj);
         lds_wait<3>(ring[j]);
         acc = fma(-ring[j], zs, acc);
-        lds_ld64(ring[j], addr(sj - 4));
+        lds_ld1(ring[j], addr(sj - 4));
       });
     }
     lds_wait<0>(ring[0]);   // drain the ring (its last loads are dummies)
@@ -392,33 +418,33 @@ __device__ __forceinline__ double tri_bwd(double acc, const double* Mc, const do
     static_assert(L::W == 2 && NV > 64, "two-wave sweeps only");
     // as in tri_fwd_lds: each wave sweeps all rows (lane, lane + 64)
     const int lane = tid & 63;
-    double a0, a1;
+    real a0, a1;
     sweep_stage(acc, a0, a1, red);
     const unsigned b0 = lds_addr(Mc + L::cb(lane) - lane);
     const unsigned b1 = lds_addr(Mc + (lane + 64 < NV ? L::cb(lane + 64) - (lane + 64) : 0));
     const unsigned zaddr = lds_addr(zero);
-    auto ad0 = [&](int s) -> unsigned { return (lane < s && s < NV && s >= 0) ? b0 + 8u * (unsigned)s : zaddr; };
+    auto ad0 = [&](int s) -> unsigned { return (lane < s && s < NV && s >= 0) ? b0 + (unsigned)RB * (unsigned)s : zaddr; };
     auto ad1 = [&](int s) -> unsigned {
-      return (lane + 64 < s && s < NV && s >= 0) ? b1 + 8u * (unsigned)s : zaddr;
+      return (lane + 64 < s && s < NV && s >= 0) ? b1 + (unsigned)RB * (unsigned)s : zaddr;
     };
     constexpr int RD = kRing2;
     constexpr int STOP2 = ((NV + RD - 1) / RD) * RD - 1;   // first step, padded to the ring
-    double r0[RD], r1[RD];
+    real r0[RD], r1[RD];
     sfor<0, RD>([&](auto jc) __attribute__((always_inline)) {
       constexpr int j = decltype(jc)::value;
-      lds_ld64(r0[j], ad0(STOP2 - j));
-      lds_ld64(r1[j], ad1(STOP2 - j));
+      lds_ld1(r0[j], ad0(STOP2 - j));
+      lds_ld1(r1[j], ad1(STOP2 - j));
     });
-    auto steps = [&](int s, const double& src, int off) __attribute__((always_inline)) {
+    auto steps = [&](int s, const real& src, int off) __attribute__((always_inline)) {
       sfor<0, RD>([&](auto jc) __attribute__((always_inline)) {
         constexpr int j = decltype(jc)::value;
         const int sj = s - j;
-        const double zs = rdlane(src, sj - off);
+        const real zs = rdlane(src, sj - off);
         lds_wait<2 * RD - 2>(r0[j], r1[j]);
         a0 = fma(-r0[j], zs, a0);
         a1 = fma(-r1[j], zs, a1);
-        lds_ld64(r0[j], ad0(sj - RD));
-        lds_ld64(r1[j], ad1(sj - RD));
+        lds_ld1(r0[j], ad0(sj - RD));
+        lds_ld1(r1[j], ad1(sj - RD));
       });
     };
 #pragma unroll 1
@@ -455,18 +481,19 @@ __device__ __forceinline__ double tri_bwd(double acc, const double* Mc, const do
 #ifndef HMPC_WAVES_PER_EU
 #define HMPC_WAVES_PER_EU(W) ((W) == 1 ? 2 : 1)
 #endif
-template <int VAR, int N>
+template <int VAR, int N, typename R>
 __global__ void __launch_bounds__(Lay<N>::NT, HMPC_WAVES_PER_EU(Lay<N>::W))
 solve_kernel(SolveArgs a) {
+  static_assert(sizeof(R) == sizeof(real), "one arithmetic type per build");
   using L = Lay<N>;
   constexpr int NV = L::NV;
   constexpr int W = L::W;
   constexpr int NT = L::NT;
   constexpr int QMAX = L::QMAX;
   using B = Blk<W>;
-  __shared__ __attribute__((aligned(16))) double sm[L::TOTAL];
-  double* red = sm + L::RED;
-  double* xs = sm + L::XS;
+  __shared__ __attribute__((aligned(16))) real sm[L::TOTAL];
+  real* red = sm + L::RED;
+  real* xs = sm + L::XS;
 #ifdef HMPC_STAMPS
   long long stamp_[16] = {0};
 #endif
@@ -474,8 +501,8 @@ solve_kernel(SolveArgs a) {
 
   const int tid = threadIdx.x;
   const int64_t b = blockIdx.x;
-  const double dt = a.dt;
-  const double dtm = dt / a.m;
+  const real dt = a.dt;
+  const real dtm = dt / real(a.m);
 
   // ---------------- phase 0: coalesced loads --------------------------------
   // x_ref / pf / C may be strided views (a resident plan, path_plan_grab
@@ -483,7 +510,7 @@ solve_kernel(SolveArgs a) {
   const double* xrf = a.x_ref + b * a.xref_bs;
   if (tid == 0) {   // kept in LDS, not in SGPRs, until phase 7 reads x_ref again
     reinterpret_cast<const double**>(sm + L::XRV)[0] = xrf;
-    reinterpret_cast<int*>(sm + L::XRV + 1)[0] = a.xref_rs;
+    reinterpret_cast<int*>(sm + L::XRV + 2)[0] = a.xref_rs;
   }
   // Every global load is issued before the first LDS store (one memory
   // round trip instead of one per array); out-of-range lanes load element 0
@@ -492,7 +519,7 @@ solve_kernel(SolveArgs a) {
     constexpr int NR = (12 * N + NT - 1) / NT, NP = (3 * N + NT - 1) / NT, NCC = (N + NT - 1) / NT;
     const double* xp = a.x_lin + b * 12 * (N + 1);
     const int mode = a.shift_mode;
-    double vi, vr[NR], vp[NP], vc[NCC], vl[NR];
+    real vi, vr[NR], vp[NP], vc[NCC], vl[NR];
     vi = a.x_in[b * 12 + (tid < 12 ? tid : 0)];
     sfor<0, NR>([&](auto itc) __attribute__((always_inline)) {
       constexpr int it = decltype(itc)::value;
@@ -515,7 +542,7 @@ solve_kernel(SolveArgs a) {
       const int i = tid + it * NT;
       vc[it] = a.C[b * a.C_bs + (i < N ? i : 0)];
     });
-    const double mu_b = a.mu ? a.mu[b] : a.mu_default;
+    const real mu_b = a.mu ? a.mu[b] : a.mu_default;
     if (tid < 12) sm[L::XIN + tid] = vi;
     if (tid == 0) sm[L::ZR + 1] = mu_b;   // read again in phase 6
     sfor<0, NR>([&](auto itc) __attribute__((always_inline)) {
@@ -550,18 +577,18 @@ solve_kernel(SolveArgs a) {
   // more scratch in this kernel)
   if (tid < N) {
     const int k = tid;
-    const double psi = sm[L::XLIN + 12 * k + 5];
-    double sp, cp;
-    sincos(psi, &sp, &cp);
+    const real psi = sm[L::XLIN + 12 * k + 5];
+    real sp, cp;
+    sincos_r(psi, &sp, &cp);
     // rz(psi) = [[c, s, 0], [-s, c, 0], [0, 0, 1]]   (src/utils.py:46-51)
-    const double Rz[3][3] = {{cp, sp, 0.0}, {-sp, cp, 0.0}, {0.0, 0.0, 1.0}};
-    double d[3], rf[3];
+    const real Rz[3][3] = {{cp, sp, 0.0}, {-sp, cp, 0.0}, {0.0, 0.0, 1.0}};
+    real d[3], rf[3];
 #pragma unroll
     for (int i = 0; i < 3; ++i) d[i] = sm[L::PF + 3 * k + i] - sm[L::XLIN + 12 * k + i];
     // rf = rh + Rz (pf - p)   (:84)
 #pragma unroll
-    for (int i = 0; i < 3; ++i) rf[i] = a.rh[i] + (Rz[i][0] * d[0] + Rz[i][1] * d[1] + Rz[i][2] * d[2]);
-    double T[3][3], Jw[3][3], RzT[3][3];
+    for (int i = 0; i < 3; ++i) rf[i] = real(a.rh[i]) + (Rz[i][0] * d[0] + Rz[i][1] * d[1] + Rz[i][2] * d[2]);
+    real T[3][3], Jw[3][3], RzT[3][3];
 #pragma unroll
     for (int i = 0; i < 3; ++i)
 #pragma unroll
@@ -571,18 +598,18 @@ solve_kernel(SolveArgs a) {
     for (int i = 0; i < 3; ++i)
 #pragma unroll
       for (int j = 0; j < 3; ++j)
-        T[i][j] = Rz[i][0] * a.Jinv[0 * 3 + j] + Rz[i][1] * a.Jinv[1 * 3 + j] + Rz[i][2] * a.Jinv[2 * 3 + j];
+        T[i][j] = Rz[i][0] * real(a.Jinv[0 * 3 + j]) + Rz[i][1] * real(a.Jinv[1 * 3 + j]) + Rz[i][2] * real(a.Jinv[2 * 3 + j]);
 #pragma unroll
     for (int i = 0; i < 3; ++i)
 #pragma unroll
       for (int j = 0; j < 3; ++j) Jw[i][j] = T[i][0] * RzT[0][j] + T[i][1] * RzT[1][j] + T[i][2] * RzT[2][j];
-    double Bwt[3][3], Bwf[3][3];
+    real Bwt[3][3], Bwf[3][3];
     // B[9:12, 3:6] = J_w_inv Rz'   (:89)
 #pragma unroll
     for (int i = 0; i < 3; ++i)
 #pragma unroll
       for (int j = 0; j < 3; ++j) Bwt[i][j] = Jw[i][0] * RzT[0][j] + Jw[i][1] * RzT[1][j] + Jw[i][2] * RzT[2][j];
-    double w[3];
+    real w[3];
     if constexpr (VAR == 3) {   // rhat = hat(Rz' rf); B[9:12,0:3] = Jw rhat   (:85,88)
 #pragma unroll
       for (int i = 0; i < 3; ++i) w[i] = RzT[i][0] * rf[0] + RzT[i][1] * rf[1] + RzT[i][2] * rf[2];
@@ -591,7 +618,7 @@ solve_kernel(SolveArgs a) {
       for (int i = 0; i < 3; ++i) w[i] = rf[i];
     }
     // hat (src/utils.py:21-25)
-    const double hw[3][3] = {{0.0, -w[2], w[1]}, {w[2], 0.0, -w[0]}, {-w[1], w[0], 0.0}};
+    const real hw[3][3] = {{0.0, -w[2], w[1]}, {w[2], 0.0, -w[0]}, {-w[1], w[0], 0.0}};
 #pragma unroll
     for (int i = 0; i < 3; ++i)
 #pragma unroll
@@ -601,7 +628,7 @@ solve_kernel(SolveArgs a) {
         else
           Bwf[i][j] = Bwt[i][0] * hw[0][j] + Bwt[i][1] * hw[1][j] + Bwt[i][2] * hw[2][j];
       }
-    double* bw = sm + L::BW + 18 * k;
+    real* bw = sm + L::BW + 18 * k;
 #pragma unroll
     for (int i = 0; i < 3; ++i)
 #pragma unroll
@@ -621,9 +648,9 @@ solve_kernel(SolveArgs a) {
     //   free response (lane r < 12 holds xbar[r]) xbar_{k+1} = Ad_k xbar_k + Gd,
     //     d_{k+1} = W_k (xbar_{k+1} - r_k)
     //   cost-to-go (wave-uniform) S_N = W_{N-1} = 100 Q, S_t = Q + Ad_t' S_{t+1} Ad_t
-    double xr = tid < 12 ? sm[L::XIN + tid] : 0.0;
-    const double qr = qdiag(tid);
-    double s[22];
+    real xr = tid < 12 ? sm[L::XIN + tid] : 0.0;
+    const real qr = qdiag(tid);
+    real s[22];
 #pragma unroll
     for (int a3 = 0; a3 < 3; ++a3) {
       s[3 * a3] = kTermQ * kQ[a3];
@@ -643,42 +670,42 @@ solve_kernel(SolveArgs a) {
     // recursions' chains).  Both loops are unrolled: the reference rows are
     // loaded up front and the gradient terms d_t stay in registers (lane
     // r < 12: component r), so no load sits inside a recursion.
-    const double cpl = tid < N ? sm[L::CS + 2 * tid] : 0.0;
-    const double spl = tid < N ? sm[L::CS + 2 * tid + 1] : 0.0;
-    double xrf[N], dgv[N];
+    const real cpl = tid < N ? sm[L::CS + 2 * tid] : 0.0;
+    const real spl = tid < N ? sm[L::CS + 2 * tid + 1] : 0.0;
+    real xrf[N], dgv[N];
     sfor<0, N>([&](auto kc) __attribute__((always_inline)) {
       constexpr int k = decltype(kc)::value;
       xrf[k] = sm[L::XREF + 12 * k + (tid < 12 ? tid : 0)];
     });
     sfor<0, N>([&](auto kc) __attribute__((always_inline)) {
       constexpr int k = decltype(kc)::value;
-      const double cp = rdlane(cpl, k), sp = rdlane(spl, k);
-      xr = ad_lane(xr, dt, cp, sp) + ((tid == 8) ? -a.g * dt : 0.0);
-      const double kf = (k == N - 1) ? kTermQ : 1.0;
+      const real cp = rdlane(cpl, k), sp = rdlane(spl, k);
+      xr = ad_lane(xr, dt, cp, sp) + ((tid == 8) ? -real(a.g) * dt : real(0));
+      const real kf = (k == N - 1) ? kTermQ : 1.0;
       dgv[k] = kf * qr * (xr - xrf[k]);   // 0 on lanes >= 12 (qr = 0)
       if (tid == 2) sm[L::ZB + k + 1] = xr;
       constexpr int t = N - 1 - k;
       if constexpr (t >= 1) {
-        const double ct = rdlane(cpl, t), st = rdlane(spl, t);
+        const real ct = rdlane(cpl, t), st = rdlane(spl, t);
         // translational axes and yaw: [[a, b], [b, c]] with p' = p + dt v
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int o = 3 * q;
-          const double aa = s[o], bb = s[o + 1], cc = s[o + 2];
+          const real aa = s[o], bb = s[o + 1], cc = s[o + 2];
           s[o + 1] = fma(dt, aa, bb);
-          s[o + 2] = cc + dt * (2.0 * bb + dt * aa);
+          s[o + 2] = cc + dt * (real(2) * bb + dt * aa);
         }
         // roll/pitch block, theta' = theta + D w with D = dt [[c, s], [-s, c]]:
         //   M' = M + P D,   Qm' = Qm + D'(M + P D) + M' D   (old M in the last term)
-        const double D00 = ct * dt, D01 = st * dt, D10 = -st * dt, D11 = ct * dt;
-        const double P00 = s[12], P01 = s[13], P11 = s[14];
-        const double M00 = s[15], M01 = s[16], M10 = s[17], M11 = s[18];
-        const double N00 = M00 + (P00 * D00 + P01 * D10), N01 = M01 + (P00 * D01 + P01 * D11);
-        const double N10 = M10 + (P01 * D00 + P11 * D10), N11 = M11 + (P01 * D01 + P11 * D11);
-        const double A00 = D00 * N00 + D10 * N10, A01 = D00 * N01 + D10 * N11;
-        const double A11 = D01 * N01 + D11 * N11;
-        const double B00 = M00 * D00 + M10 * D10, B01 = M00 * D01 + M10 * D11;
-        const double B11 = M01 * D01 + M11 * D11;
+        const real D00 = ct * dt, D01 = st * dt, D10 = -st * dt, D11 = ct * dt;
+        const real P00 = s[12], P01 = s[13], P11 = s[14];
+        const real M00 = s[15], M01 = s[16], M10 = s[17], M11 = s[18];
+        const real N00 = M00 + (P00 * D00 + P01 * D10), N01 = M01 + (P00 * D01 + P01 * D11);
+        const real N10 = M10 + (P01 * D00 + P11 * D10), N11 = M11 + (P01 * D01 + P11 * D11);
+        const real A00 = D00 * N00 + D10 * N10, A01 = D00 * N01 + D10 * N11;
+        const real A11 = D01 * N01 + D11 * N11;
+        const real B00 = M00 * D00 + M10 * D10, B01 = M00 * D01 + M10 * D11;
+        const real B11 = M01 * D01 + M11 * D11;
         s[19] += A00 + B00;
         s[20] += A01 + B01;
         s[21] += A11 + B11;
@@ -701,7 +728,7 @@ solve_kernel(SolveArgs a) {
     // adjoint a_N = d_N, a_t = d_t + Ad_t' a_{t+1} (lane-parallel): the
     // gradient of the tracking cost w.r.t. x_t.  Only rows 6..11 are kept
     // (the nonzero rows of Bd).
-    double ar = dgv[N - 1];
+    real ar = dgv[N - 1];
     if (tid >= 6 && tid < 12) sm[L::AJ + 6 * (N - 1) + tid - 6] = ar;
     sfor<1, N>([&](auto ic) __attribute__((always_inline)) {
       constexpr int t = N - decltype(ic)::value;   // N-1 .. 1
@@ -715,24 +742,24 @@ solve_kernel(SolveArgs a) {
   // ---------------- phase 3: Hessian row (lower part) + gradient ------------
   const int vj3 = tid / 6, vc3 = tid - 6 * (tid / 6);   // stage / component of my variable
   const bool active_lane = tid < NV;
-  const double ubar_z_alias = (sm[L::CC + N - 1] != 0.0) ? 2.0 * a.m * a.g : 0.0;
+  const real ubar_z_alias = (sm[L::CC + N - 1] != 0.0) ? 2.0 * a.m * a.g : 0.0;
   auto is_fixed = [&](int k, int c) -> bool {   // swing f = 0 (:134-136), 2f fy = 0 (2f :129)
     return (c < 3 && sm[L::CC + k] == 0.0) || (VAR == 2 && c == 1);
   };
   const bool my_fixed = active_lane && is_fixed(vj3, vc3);
 
-  double Rg[NV];   // row `tid` of H (lower part), then the Cholesky trailing row
-  double hv = 0.0;
+  real Rg[NV];   // row `tid` of H (lower part), then the Cholesky trailing row
+  real hv = 0.0;
   {
     const int ii = active_lane ? vj3 : 0;
     const int ci = active_lane ? vc3 : 0;
     // my impulse b = Bd_i e_c (rows 6..11) and f = S_{i+1} b; zero for fixed
     // variables and idle lanes, whose rows of H are then zero (their unit
     // diagonal is added at the pivot, as is every 2 V_i: phase 4)
-    const double rowm = (active_lane && !my_fixed) ? 1.0 : 0.0;
-    const double cpi = sm[L::CS + 2 * ii], spi = sm[L::CS + 2 * ii + 1];
-    const double* bwi = sm + L::BW + 18 * ii;
-    double e0[12], f[12];
+    const real rowm = (active_lane && !my_fixed) ? 1.0 : 0.0;
+    const real cpi = sm[L::CS + 2 * ii], spi = sm[L::CS + 2 * ii + 1];
+    const real* bwi = sm + L::BW + 18 * ii;
+    real e0[12], f[12];
 #pragma unroll
     for (int r = 0; r < 6; ++r) e0[r] = 0.0;
 #pragma unroll
@@ -741,7 +768,7 @@ solve_kernel(SolveArgs a) {
     for (int r = 0; r < 3; ++r) e0[9 + r] = rowm * bwi[6 * r + ci];
     s_times(sm + L::SS + 22 * ii, e0, f);
     // gradient: h_v = 2 b' a_{i+1} (b = Bd_i e_c, a = adjoint of phase 2)
-    double hacc = 0.0;
+    real hacc = 0.0;
 #pragma unroll
     for (int r = 0; r < 6; ++r) hacc = fma(e0[6 + r], sm[L::AJ + 6 * ii + r], hacc);
     // H[v, (j, c2)] = 2 Bd_j[:,c2]' g_j with g_i = f, g_j = Ad_{j+1}' g_{j+1}
@@ -749,29 +776,29 @@ solve_kernel(SolveArgs a) {
     // column k from lanes >= k and overwrites register k), so entries right
     // of the diagonal keep whatever finite value falls out; the diagonal
     // block needs no special case (its 2 V_i goes in at the pivot).
-    double g[12];
+    real g[12];
 #pragma unroll
     for (int r = 0; r < 12; ++r) g[r] = f[r];
     sfor<0, N>([&](auto jc) __attribute__((always_inline)) {
       constexpr int j = N - 1 - decltype(jc)::value;
-      const double* smj = sm + opaque_zero();   // keeps this step's loads here
+      const real* smj = sm + opaque_zero();   // keeps this step's loads here
       if constexpr (j < N - 1) {
-        const double cp1 = smj[L::CS + 2 * (j + 1)], sp1 = smj[L::CS + 2 * (j + 1) + 1];
-        double gn[12];
+        const real cp1 = smj[L::CS + 2 * (j + 1)], sp1 = smj[L::CS + 2 * (j + 1) + 1];
+        real gn[12];
 #pragma unroll
         for (int r = 0; r < 12; ++r) gn[r] = g[r];
         adt_times(gn, dt, cp1, sp1);
 #pragma unroll
         for (int r = 0; r < 12; ++r) g[r] = (ii > j) ? gn[r] : g[r];
       }
-      const double cp = smj[L::CS + 2 * j], sp = smj[L::CS + 2 * j + 1];
-      const double* bw = smj + L::BW + 18 * j;
+      const real cp = smj[L::CS + 2 * j], sp = smj[L::CS + 2 * j + 1];
+      const real* bw = smj + L::BW + 18 * j;
       // fixed columns (swing forces :134-136) of stage j: zero
-      const double stance_j = smj[L::CC + j] != 0.0 ? 1.0 : 0.0;
+      const real stance_j = smj[L::CC + j] != 0.0 ? 1.0 : 0.0;
       sfor<0, 6>([&](auto c2c) __attribute__((always_inline)) {
         constexpr int c2 = decltype(c2c)::value;
         constexpr int w = 6 * j + c2;
-        double val;
+        real val;
         if constexpr (VAR == 2 && c2 == 1) val = 0.0;   // 2f fy (2f :129)
         else if constexpr (c2 < 3) val = stance_j * bd_dot<VAR>(c2, g, bw, dtm, cp, sp);
         else val = bd_dot<VAR>(c2, g, bw, dtm, cp, sp);
@@ -780,21 +807,21 @@ solve_kernel(SolveArgs a) {
       });
     });
     if (active_lane && !my_fixed) {
-      double ub = 0.0;
+      real ub = 0.0;
       if (vc3 == 2) ub = a.uref_aliased ? ubar_z_alias : ((sm[L::CC + vj3] != 0.0) ? 2.0 * a.m * a.g : 0.0);
-      const double Vj = (vj3 == N - 1) ? 0.0 : kRdiag;
-      hv = 2.0 * hacc - 2.0 * Vj * ub;
+      const real Vj = (vj3 == N - 1) ? 0.0 : kRdiag;
+      hv = real(2) * hacc - real(2) * Vj * ub;
     }
   }
-  double wv = -hv;   // the forward sweep's accumulator (phase 4)
+  real wv = -hv;   // the forward sweep's accumulator (phase 4)
   __syncthreads();   // union A (XLIN/XREF/PF/S/DG) is dead from here on
   HMPC_STAMP(4);
 
   int status = ST_SOLVED;
-  double dinv = 0.0;
+  real dinv = 0.0;
   // the diagonal of H not built in phase 3: 1 for a fixed variable (identity
   // row/column), else 2 V_i (R * kuf: every stage but the last, 3f :114,132,139)
-  auto diag_extra = [&](int k, bool fixed) -> double {
+  auto diag_extra = [&](int k, bool fixed) -> real {
     return fixed ? 1.0 : ((k / 6 != N - 1) ? 2.0 * kRdiag : 0.0);
   };
 
@@ -814,7 +841,7 @@ solve_kernel(SolveArgs a) {
     if (tid == 0) sm[L::ZR] = 0.0;
     // non-positive pivots, counted: `if (piv <= 0) status = ...` per step
     // kept 60 condition masks alive in SGPRs (and spilled)
-    double nbad = 0.0;
+    real nbad = 0.0;
     auto nld_of = [](int lo, int ch) constexpr {   // b128 loads of chunk ch of [lo, NV)
       return (NV - lo - 8 * ch) >= 8 ? 4 : (NV - lo - 8 * ch + 1) / 2;
     };
@@ -832,16 +859,16 @@ solve_kernel(SolveArgs a) {
                                          : ((NV - ja - CW * ch) > 0 ? (NV - ja - CW * ch + 1) / 2 : 0);
       };
       const uint64_t fixmask = __ballot(active_lane && is_fixed(vj3, vc3));
-      const double dx = diag_extra(tid, my_fixed);   // lane s: the extra of pivot s
-      dbl2 nb[CW / 2];                 // chunk 0 of the next step
-      double p_rs = 0.0, p_tk = 0.0;   // next step's 1/L_kk and M[tid][k]
+      const real dx = diag_extra(tid, my_fixed);   // lane s: the extra of pivot s
+      real2 nb[CW / 2];                 // chunk 0 of the next step
+      real p_rs = 0.0, p_tk = 0.0;   // next step's 1/L_kk and M[tid][k]
       auto ahead = [&](auto sc) __attribute__((always_inline)) {
         constexpr int s = decltype(sc)::value;
         constexpr int JS = (s + 1) & ~1;
         // lane masks of a step come from an opaque copy of its index: hoisted
         // out of the unrolled steps they would pin ~100 SGPRs (and spill)
-        double* col = sm + L::COLB + (s & 1) * (NT + 8);
-        const double mine = Rg[s];
+        real* col = sm + L::COLB + (s & 1) * (NT + 8);
+        const real mine = Rg[s];
         // unmasked: the updates read rows > s only (lanes < s hold
         // don't-care upper-triangle values there, lanes >= NV are never read)
         col[tid] = mine;
@@ -849,11 +876,11 @@ solve_kernel(SolveArgs a) {
         const unsigned cb0 = lds_addr(col + JS);
         sfor<0, nldc(JS, 0)>([&](auto ic) __attribute__((always_inline)) {
           constexpr int i = decltype(ic)::value;
-          lds_ld128<16 * i>(nb[i], cb0);
+          lds_ld2<2 * RB * i>(nb[i], cb0);
         });
-        const double piv = rdlane(mine + dx, s);
-        const double pv = piv > 0.0 ? piv : 1.0;
-        nbad += (piv > 0.0) ? 0.0 : 1.0;   // folded into status after the loop
+        const real piv = rdlane(mine + dx, s);
+        const real pv = piv > 0.0 ? piv : 1.0;
+        nbad += (piv > real(0)) ? real(0) : real(1);   // folded into status after the loop
         pin(nbad);                          // (materialised here, not sunk to the end)
         p_rs = rsq_nr(pv);
         p_tk = (mine * p_rs) * p_rs;
@@ -867,12 +894,12 @@ solve_kernel(SolveArgs a) {
         constexpr bool kfixed = VAR == 2 && k % 6 == 1;                       // 2f fy
         constexpr bool kforce = k % 6 < 3;
         const int ko = k + opaque_zero();
-        const double rs = p_rs, tk = p_tk;
+        const real rs = p_rs, tk = p_tk;
         lds_wait<0>(nb[0], nb[1]);   // this step's chunk 0 (and everything older)
         const bool below = tid > ko && tid < NV;
         // every lane updates: a lane <= k changes only its registers > k, the
         // upper triangle of its row (don't-care, overwritten at their step)
-        const double nt = -tk;
+        const real nt = -tk;
         // branch-free store of column k of M (other lanes: the column buffer
         // of step k+1, which ahead() rewrites after this store)
         {
@@ -886,13 +913,13 @@ solve_kernel(SolveArgs a) {
         const unsigned cbase = lds_addr(sm + L::COLB + (k & 1) * (NT + 8) + JA);
         // chunks >= 1 go through a 3-deep ring: chunk ch+2 is issued while
         // chunk ch is consumed (one chunk ahead left the LDS latency exposed)
-        dbl2 buf[3][CW / 2];
+        real2 buf[3][CW / 2];
         auto load = [&](auto chc) __attribute__((always_inline)) {
           constexpr int ch = decltype(chc)::value;
           if constexpr (ch >= 1 && ch < NCH) {
             sfor<0, nldc(JA, ch)>([&](auto ic) __attribute__((always_inline)) {
               constexpr int i = decltype(ic)::value;
-              lds_ld128<8 * CW * ch + 16 * i>(buf[ch % 3][i], cbase);
+              lds_ld2<RB * (CW * ch + 2 * i)>(buf[ch % 3][i], cbase);
             });
           }
         };
@@ -901,13 +928,13 @@ solve_kernel(SolveArgs a) {
                                                                  : (NV - ja - CW * ch + 1) / 2)
                                                            : 0;
         };
-        auto update = [&](auto chc, const dbl2 (&bf)[CW / 2]) __attribute__((always_inline)) {
+        auto update = [&](auto chc, const real2 (&bf)[CW / 2]) __attribute__((always_inline)) {
           constexpr int ch = decltype(chc)::value;
           sfor<0, CW>([&](auto ic) __attribute__((always_inline)) {
             constexpr int i = decltype(ic)::value;
             constexpr int j = JA + CW * ch + i;
             if constexpr (j > k && j < NV) {
-              const double cv = (i & 1) ? bf[i / 2].y : bf[i / 2].x;
+              const real cv = (i & 1) ? bf[i / 2].y : bf[i / 2].x;
               Rg[j] = fma(nt, cv, Rg[j]);
               pin(Rg[j]);
             }
@@ -939,11 +966,11 @@ solve_kernel(SolveArgs a) {
         }
       });
     } else {
-      double mine = Rg[0];   // A[tid][k] of the current step
+      real mine = Rg[0];   // A[tid][k] of the current step
       // pivot extras (diag_extra) by lane, behind the column buffers (the
       // active-set state there is not live yet); the first step's barrier
       // publishes them
-      double* dxa = sm + L::COLB + 2 * (NT + 8);
+      real* dxa = sm + L::COLB + 2 * (NT + 8);
       static_assert(L::COLB + 2 * (NT + 8) + NT <= L::U0, "pivot extras do not fit");
       dxa[tid] = diag_extra(tid, my_fixed);
       sfor<0, (NV + 7) / 8>([&](auto bc) __attribute__((always_inline)) {
@@ -953,36 +980,36 @@ solve_kernel(SolveArgs a) {
         constexpr int NCH = (NV - J0 + 7) / 8;
 #pragma unroll 1
         for (int k = J0; k < KEND; ++k) {
-          double* col = sm + L::COLB + (k & 1) * (NT + 8);
+          real* col = sm + L::COLB + (k & 1) * (NT + 8);
           col[tid] = (tid >= k && tid < NV) ? mine : 0.0;
           if (tid == k) col[NT] = wv;   // w_k (final) for the riding forward sweep
           B::sync();
-          const double piv = col[k] + dxa[k];
-          const double wk = col[NT];
+          const real piv = col[k] + dxa[k];
+          const real wk = col[NT];
           const unsigned cbase = lds_addr(col + J0);
-          dbl2 buf[2][4];
+          real2 buf[2][4];
           auto load = [&](auto chc) __attribute__((always_inline)) {
             constexpr int ch = decltype(chc)::value;
             if constexpr (ch < NCH) {
               sfor<0, nld_of(J0, ch)>([&](auto ic) __attribute__((always_inline)) {
                 constexpr int i = decltype(ic)::value;
-                lds_ld128<64 * ch + 16 * i>(buf[ch % 2][i], cbase);
+                lds_ld2<RB * (8 * ch + 2 * i)>(buf[ch % 2][i], cbase);
               });
             }
           };
           load(std::integral_constant<int, 0>{});
-          const double pv = piv > 0.0 ? piv : 1.0;
-          nbad += (piv > 0.0) ? 0.0 : 1.0;   // folded into status after the loop
+          const real pv = piv > 0.0 ? piv : 1.0;
+          nbad += (piv > real(0)) ? real(0) : real(1);   // folded into status after the loop
         pin(nbad);                          // (materialised here, not sunk to the end)
-          const double rs = rsq_nr(pv);
-          const double tk = (mine * rs) * rs;
+          const real rs = rsq_nr(pv);
+          const real tk = (mine * rs) * rs;
           const bool below = tid > k && tid < NV;
-          const double mk = below ? tk : 0.0;
+          const real mk = below ? tk : 0.0;
           wv = fma(-mk, wk, wv);   // phase 5's forward substitution (as one wave)
           // unmasked: the published column is 0 above row k, so a lane <= k
           // changes only its upper triangle (registers > k, never read)
-          const double nt = -tk;
-          double nxt = 0.0;
+          const real nt = -tk;
+          real nxt = 0.0;
           sfor<0, NCH>([&](auto chc) __attribute__((always_inline)) {
             constexpr int ch = decltype(chc)::value;
             load(std::integral_constant<int, ch + 1>{});
@@ -992,8 +1019,8 @@ solve_kernel(SolveArgs a) {
               constexpr int i = decltype(ic)::value;
               constexpr int j = J0 + 8 * ch + i;
               if constexpr (j < NV) {
-                const double cv = (i & 1) ? buf[ch % 2][i / 2].y : buf[ch % 2][i / 2].x;
-                double r = fma(nt, cv, Rg[j]);
+                const real cv = (i & 1) ? buf[ch % 2][i / 2].y : buf[ch % 2][i / 2].x;
+                real r = fma(nt, cv, Rg[j]);
                 if constexpr (j < KEND) r = (j == k) ? mk : r;
                 Rg[j] = r;
                 pin(Rg[j]);
@@ -1015,13 +1042,13 @@ solve_kernel(SolveArgs a) {
   }
   HMPC_STAMP(5);
 
-  const double* Lc = sm + L::LC;
-  const double* zero = sm + L::ZR;
+  const real* Lc = sm + L::LC;
+  const real* zero = sm + L::ZR;
 
   // ---------------- phase 5: v0 = -L^-T L^-1 h -------------------------------
-  double v = 0.0;
+  real v = 0.0;
   {
-    double y;
+    real y;
     y = wv * dinv;   // L^-1 (-h), swept during the Cholesky
     v = tri_bwd<N>(y, Lc, zero, dinv, xs);
   }
@@ -1029,8 +1056,8 @@ solve_kernel(SolveArgs a) {
 
   // per-instance scalars needed after the factorisation are re-derived here
   // rather than kept live across it (they were spilled there)
-  const double mu = sm[L::ZR + 1];   // staged in phase 0
-  const double dtm2 = dt / a.m + 0.0 * (double)opaque_zero();
+  const real mu = sm[L::ZR + 1];   // staged in phase 0
+  const real dtm2 = dt / real(a.m) + real(0) * (real)opaque_zero();
   // stage / component of my variable, recomputed from an opaque thread id:
   // phase 3's copies would stay alive (spilled) across the factorisation
   const int tid_o = tid + opaque_zero();
@@ -1045,12 +1072,12 @@ solve_kernel(SolveArgs a) {
   //   c in 0..1 : slot0 -f + mu fz >= 0, slot1 f + mu fz >= 0   (:141-144)
   //   (stance only for c <= 2; 2f has no fy rows)
   int iters = 0;
-  const double zmin_gap_k0 = sm[L::XIN + 2] - kZmin;    // z_0 row: constant
-  const double zmin_gap_k1 = sm[L::ZB + 1] - kZmin;     // z_1 row: constant
-  if (zmin_gap_k0 < -kTol || zmin_gap_k1 < -kTol) status = ST_INFEAS;
+  const real zmin_gap_k0 = sm[L::XIN + 2] - real(kZmin);    // z_0 row: constant
+  const real zmin_gap_k1 = sm[L::ZB + 1] - kZmin;     // z_1 row: constant
+  if (zmin_gap_k0 < -kTolR || zmin_gap_k1 < -kTolR) status = ST_INFEAS;
   // coefficient of fz_j in z_k (j <= k-2): dt * (dt/m) * (k-1-j), stance only
   // (Bd[8][2] = dt/m in both variants)
-  const double zc = dt * dtm2;
+  const real zc = dt * dtm2;
 
   const bool stance_me = active_lane && vc <= 2 && sm[L::CC + vj] != 0.0;
   int nslots = 0;
@@ -1060,16 +1087,16 @@ solve_kernel(SolveArgs a) {
   }
   // |n| of my z row (stance stages j <= k-2): a uniform, unrolled masked sum
   // (a per-lane loop would diverge and wait on one LDS load per trip)
-  double s2 = 0.0;
+  real s2 = 0.0;
   sfor<0, (N > 2 ? N - 2 : 0)>([&](auto jc) __attribute__((always_inline)) {
     constexpr int j = decltype(jc)::value;
-    const double cz = zc * (double)(vj - 1 - j);
-    const double m = (j <= vj - 2 && sm[L::CC + j] != 0.0) ? 1.0 : 0.0;
+    const real cz = zc * (real)(vj - 1 - j);
+    const real m = (j <= vj - 2 && sm[L::CC + j] != 0.0) ? 1.0 : 0.0;
     s2 = fma(m * cz, cz, s2);
   });
-  const double znorm = (active_lane && vc == 3 && vj >= 2) ? sqrt(s2) : 0.0;
+  const real znorm = (active_lane && vc == 3 && vj >= 2) ? sqrt(s2) : 0.0;
   // slot 0/1 coefficients of my constraints (see the table above)
-  double a0 = 1.0, muf = 0.0, k0 = 0.0, k1 = 0.0, inv01 = 1.0;
+  real a0 = 1.0, muf = 0.0, k0 = 0.0, k1 = 0.0, inv01 = 1.0;
   if (vc >= 3) {
     k0 = k1 = tau_lim(vc);
   } else if (vc == 2) {
@@ -1077,24 +1104,24 @@ solve_kernel(SolveArgs a) {
   } else {
     a0 = -1.0;
     muf = mu;
-    inv01 = 1.0 / sqrt(1.0 + mu * mu);
+    inv01 = real(1) / sqrt(real(1) + mu * mu);
   }
   int actmask = 0;
 
-  double* Rm = sm + L::RM;   // packed upper, column k at loff(k)
-  double* ua = sm + L::UA;
+  real* Rm = sm + L::RM;   // packed upper, column k at loff(k)
+  real* ua = sm + L::UA;
   int* act = reinterpret_cast<int*>(sm + L::ACT);
-  double* cbv = sm + L::CB;
-  double* gv = sm + L::GV;
-  double* sdg = sm + L::SD;
-  double Qw[QMAX];   // row `tid` of the orthonormal basis of L^-1 N_A
+  real* cbv = sm + L::CB;
+  real* gv = sm + L::GV;
+  real* sdg = sm + L::SD;
+  real Qw[QMAX];   // row `tid` of the orthonormal basis of L^-1 N_A
 #pragma unroll
   for (int l = 0; l < QMAX; ++l) Qw[l] = 0.0;
   int q = 0;
   const int max_iter = 4 * NV + 50;
 
   // coefficient of lane `i`'s variable in constraint `id`, and its rhs
-  auto coef_of = [&](int id, int i) -> double {
+  auto coef_of = [&](int id, int i) -> real {
     const int o = id >> 2, sl = id & 3, oj = o / 6, oc = o - 6 * oj;
     if (i >= NV) return 0.0;
     if (oc >= 3) {
@@ -1103,18 +1130,18 @@ solve_kernel(SolveArgs a) {
       // z-row of stage oj over fz_j, j <= oj-2
       const int ij = i / 6, ic = i - 6 * ij;
       if (ic != 2 || ij > oj - 2 || sm[L::CC + ij] == 0.0) return 0.0;
-      return zc * (double)(oj - 1 - ij);
+      return zc * (real)(oj - 1 - ij);
     }
     if (oc == 2) return i == o ? (sl == 0 ? 1.0 : -1.0) : 0.0;
     if (i == o) return sl == 0 ? -1.0 : 1.0;
     if (i == 6 * oj + 2) return mu;
     return 0.0;
   };
-  auto rhs_of = [&](int id) -> double {
+  auto rhs_of = [&](int id) -> real {
     const int o = id >> 2, sl = id & 3, oj = o / 6, oc = o - 6 * oj;
     if (oc >= 3) {
       if (sl < 2) return -tau_lim(oc);
-      return kZmin - sm[L::ZB + oj];
+      return real(kZmin) - sm[L::ZB + oj];
     }
     if (oc == 2) return sl == 0 ? 0.0 : -kFzMax;
     return 0.0;
@@ -1129,36 +1156,36 @@ solve_kernel(SolveArgs a) {
     // branch-free: slots 0/1 are +-a0 v + muf fz_stage + k0/k1; slot 2 the
     // z row ZB_k + zc ((k-1) S1 - S2) with S1 = sum C_j fz_j, S2 = sum j C_j fz_j
     // over j <= k-2 (prefix sums over a uniform trip count)
-    double z1 = 0.0, z2 = 0.0;
+    real z1 = 0.0, z2 = 0.0;
     sfor<0, (N > 2 ? N - 2 : 0)>([&](auto jc) __attribute__((always_inline)) {
       constexpr int j = decltype(jc)::value;
-      const double val = sm[L::CC + j] * xs[6 * j + 2];
-      const double msk = (j <= vj - 2) ? 1.0 : 0.0;
+      const real val = sm[L::CC + j] * xs[6 * j + 2];
+      const real msk = (j <= vj - 2) ? 1.0 : 0.0;
       z1 = fma(msk, val, z1);
-      z2 = fma(msk * (double)j, val, z2);
+      z2 = fma(msk * (real)j, val, z2);
     });
-    const double fzs = xs[6 * (active_lane ? vj : 0) + 2];
-    const double sc0 = fma(a0, v, fma(muf, fzs, k0)) * inv01;
-    const double sc1 = fma(-a0, v, fma(muf, fzs, k1)) * inv01;
-    const double zrow = (sm[L::ZB + (active_lane ? vj : 0)] - kZmin) + zc * fma((double)(vj - 1), z1, -z2);
-    const double sc2 = znorm > 0.0 ? zrow / znorm : ((zrow < -kTol) ? -INFINITY : INFINITY);
-    double best = INFINITY;
+    const real fzs = xs[6 * (active_lane ? vj : 0) + 2];
+    const real sc0 = fma(a0, v, fma(muf, fzs, k0)) * inv01;
+    const real sc1 = fma(-a0, v, fma(muf, fzs, k1)) * inv01;
+    const real zrow = (sm[L::ZB + (active_lane ? vj : 0)] - real(kZmin)) + zc * fma((real)(vj - 1), z1, -z2);
+    const real sc2 = znorm > 0.0 ? zrow / znorm : ((zrow < -kTolR) ? -INFINITY : INFINITY);
+    real best = INFINITY;
     int bid = 0x7fffffff;
     if (nslots > 0 && !(actmask & 1)) argmin_combine(best, bid, sc0, 4 * tid);
     if (nslots > 1 && !(actmask & 2)) argmin_combine(best, bid, sc1, 4 * tid + 1);
     if (nslots > 2 && !(actmask & 4)) argmin_combine(best, bid, sc2, 4 * tid + 2);
     B::argmin(best, bid, red);
     HMPC_TOC(9, t_scan);
-    if (!(best < -kTol)) break;   // primal feasible: optimal
+    if (!(best < -kTolR)) break;   // primal feasible: optimal
     const int p = uni(bid);
-    const double bp = rhs_of(p);
-    const double np_me = coef_of(p, tid);
-    double u_plus = 0.0;
+    const real bp = rhs_of(p);
+    const real np_me = coef_of(p, tid);
+    real u_plus = 0.0;
     // w = L^-1 n_p
     HMPC_TIC(t_fwd);
     const int s0 = B::first(np_me != 0.0, red);   // first nonzero of n_p (-1: none)
-    const double wfull = tri_fwd_lds<N>(np_me, Lc, zero, dinv, xs, s0 > 0 ? (s0 & ~(W == 1 ? 3 : kRing2 - 1)) : 0);
-    const double wnorm2 = B::sum(wfull * wfull, red);
+    const real wfull = tri_fwd_lds<N>(np_me, Lc, zero, dinv, xs, s0 > 0 ? (s0 & ~(W == 1 ? 3 : kRing2 - 1)) : 0);
+    const real wnorm2 = B::sum(wfull * wfull, red);
     HMPC_TOC(10, t_fwd);
 
     // ---- inner loop: step towards satisfying constraint p ----
@@ -1168,33 +1195,33 @@ solve_kernel(SolveArgs a) {
       // w_perp = (I - Qw Qw') w and c = Qw' w by modified Gram-Schmidt; a
       // second pass when the first one cancels more than half the norm
       HMPC_TIC(t_gs);
-      double wp = wfull, zn = wnorm2;
+      real wp = wfull, zn = wnorm2;
 #pragma unroll 1
       for (int pass = 0; pass < 2 && qu > 0; ++pass) {
         if constexpr (W == 1) {   // modified Gram-Schmidt: no barriers in one wave
           ladder<0, QMAX>(qu, [&](auto lc) __attribute__((always_inline)) {
             constexpr int l = decltype(lc)::value;
-            const double cl = B::sum(Qw[l] * wp, red);
+            const real cl = B::sum(Qw[l] * wp, red);
             wp = fma(-cl, Qw[l], wp);
             if (tid == 0) cbv[l] = (pass == 0) ? cl : cbv[l] + cl;
           });
         } else {   // classical Gram-Schmidt: all q projections behind one exchange
-          double* part = sm + L::GS;
+          real* part = sm + L::GS;
           ladder<0, QMAX>(qu, [&](auto lc) __attribute__((always_inline)) {
             constexpr int l = decltype(lc)::value;
-            const double pl = wave_sum(Qw[l] * wp);
+            const real pl = wave_sum(Qw[l] * wp);
             if ((tid & 63) == 0) part[(tid >> 6) * QMAX + l] = pl;
           });
           __syncthreads();
           ladder<0, QMAX>(qu, [&](auto lc) __attribute__((always_inline)) {
             constexpr int l = decltype(lc)::value;
-            const double cl = part[l] + part[QMAX + l];
+            const real cl = part[l] + part[QMAX + l];
             wp = fma(-cl, Qw[l], wp);
             if (tid == 0) cbv[l] = (pass == 0) ? cl : cbv[l] + cl;
           });
         }
-        const double n2 = B::sum(wp * wp, red);
-        const bool enough = n2 > 0.25 * zn;
+        const real n2 = B::sum(wp * wp, red);
+        const bool enough = n2 > real(0.25) * zn;
         zn = n2;
         if (enough) break;
       }
@@ -1202,26 +1229,26 @@ solve_kernel(SolveArgs a) {
       HMPC_TOC(11, t_gs);
       // primal direction z = L^-T w_perp (lane v gets z_v)
       HMPC_TIC(t_bwd);
-      const double zi = tri_bwd<N>(wp, Lc, zero, dinv, xs);
+      const real zi = tri_bwd<N>(wp, Lc, zero, dinv, xs);
       HMPC_TOC(12, t_bwd);
       HMPC_TIC(t_dual);
       // dual direction r = R^-1 c (lanes l < q), back substitution
-      double rcur = tid < qu ? cbv[tid] : 0.0, rmine = 0.0;
+      real rcur = tid < qu ? cbv[tid] : 0.0, rmine = 0.0;
       for (int l = qu - 1; l >= 0; --l) {
-        const double rl = B::bcast(rcur, l, red) / Rm[loff(l) + l];
+        const real rl = B::bcast(rcur, l, red) / Rm[loff(l) + l];
         if (tid == l) rmine = rl;
         if (tid < l) rcur = fma(-Rm[loff(l) + tid], rl, rcur);
       }
       // partial step length t1 (drop candidate)
-      double t1 = INFINITY;
+      real t1 = INFINITY;
       int kdrop = 0x7fffffff;
       if (tid < qu && rmine > 0.0) { t1 = ua[tid] / rmine; kdrop = tid; }
       B::argmin(t1, kdrop, red);
       // full step length t2 (n_p' z = |w_perp|^2)
-      const double sp_ = B::sum(np_me * v, red) - bp;
-      const bool has_z = zn > 1e-24 * wnorm2;
-      const double t2 = has_z ? -sp_ / zn : INFINITY;
-      const double t = t1 < t2 ? t1 : t2;
+      const real sp_ = B::sum(np_me * v, red) - bp;
+      const bool has_z = zn > kZnRel * wnorm2;
+      const real t2 = has_z ? -sp_ / zn : INFINITY;
+      const real t = t1 < t2 ? t1 : t2;
       if (!(t < INFINITY)) { status = ST_INFEAS; done = true; break; }
       if (has_z) v = fma(t, zi, v);
       if (tid < qu) ua[tid] -= t * rmine;
@@ -1234,8 +1261,8 @@ solve_kernel(SolveArgs a) {
         // active set beyond the register/LDS capacity: handed to the
         // overflow pass (hmpc_ric.hip, capacity NV) when the caller set one up
         if (qu >= QMAX) { status = a.ovf_count ? ST_OVERFLOW : ST_NUMERICAL; done = true; break; }
-        const double rho = sqrt(zn);
-        const double qn = wp / rho;
+        const real rho = sqrt(zn);
+        const real qn = wp / rho;
         // (selects over every register, not a branch per index: branches that
         // store to different elements get merged into one dynamically
         // indexed store, and the array lands in scratch)
@@ -1257,7 +1284,7 @@ solve_kernel(SolveArgs a) {
         if (tid == (idk >> 2)) actmask &= ~(1 << (idk & 3));
         // shift R columns k+1..q-1 left; remember the subdiagonals
         for (int m = k; m + 1 < qu; ++m) {
-          double val = 0.0;
+          real val = 0.0;
           if (tid <= m + 1) val = Rm[loff(m + 1) + tid];
           B::sync();
           if (tid <= m) Rm[loff(m) + tid] = val;
@@ -1267,7 +1294,7 @@ solve_kernel(SolveArgs a) {
         // shift the active list and multipliers
         {
           int an = 0;
-          double un = 0.0;
+          real un = 0.0;
           if (tid >= k && tid + 1 < qu) { an = act[tid + 1]; un = ua[tid + 1]; }
           B::sync();
           if (tid >= k && tid + 1 < qu) { act[tid] = an; ua[tid] = un; }
@@ -1275,14 +1302,14 @@ solve_kernel(SolveArgs a) {
         }
         // Givens to restore the triangle: rows (l, l+1), l = k..q-2
         for (int l = k; l + 1 < qu; ++l) {
-          const double aa = Rm[loff(l) + l], bb = sdg[l];
-          const double hh = sqrt(aa * aa + bb * bb);
-          const double cg = aa / hh, sg = bb / hh;
+          const real aa = Rm[loff(l) + l], bb = sdg[l];
+          const real hh = sqrt(aa * aa + bb * bb);
+          const real cg = aa / hh, sg = bb / hh;
           B::sync();
           if (tid == l) { Rm[loff(l) + l] = hh; gv[2 * l] = cg; gv[2 * l + 1] = sg; }
           const int mcol = tid;   // columns m > l hold rows l, l+1
           if (mcol > l && mcol + 1 < qu) {
-            const double rl = Rm[loff(mcol) + l], rl1 = Rm[loff(mcol) + l + 1];
+            const real rl = Rm[loff(mcol) + l], rl1 = Rm[loff(mcol) + l + 1];
             Rm[loff(mcol) + l] = cg * rl + sg * rl1;
             Rm[loff(mcol) + l + 1] = -sg * rl + cg * rl1;
           }
@@ -1293,8 +1320,8 @@ solve_kernel(SolveArgs a) {
         for (int l = 0; l + 1 < QMAX; ++l) {
           const bool rot = l >= k && l + 1 < qu;
           const int lg = rot ? l : 0;
-          const double cg = gv[2 * lg], sg = gv[2 * lg + 1];
-          const double x0 = Qw[l], x1 = Qw[l + 1];
+          const real cg = gv[2 * lg], sg = gv[2 * lg + 1];
+          const real x0 = Qw[l], x1 = Qw[l + 1];
           Qw[l] = rot ? cg * x0 + sg * x1 : x0;
           Qw[l + 1] = rot ? -sg * x0 + cg * x1 : x1;
         }
@@ -1326,8 +1353,8 @@ solve_kernel(SolveArgs a) {
   // x_ref again (its LDS copy is gone): every row's load is issued here,
   // ahead of the rollout, so no memory round trip sits inside it
   const double* xrf7 = reinterpret_cast<const double* const*>(sm + L::XRV)[0];
-  const int xrs = reinterpret_cast<const int*>(sm + L::XRV + 1)[0];
-  double xrg[N];
+  const int xrs = reinterpret_cast<const int*>(sm + L::XRV + 2)[0];
+  real xrg[N];
   sfor<0, N>([&](auto kc) __attribute__((always_inline)) {
     constexpr int k = decltype(kc)::value;
     xrg[k] = xrf7[k * xrs + (tid < 12 ? tid : 0)];
@@ -1336,42 +1363,42 @@ solve_kernel(SolveArgs a) {
   xs[tid] = v;
   __syncthreads();   // L is dead: XO aliases it
   {
-    double* xo = sm + L::XO;
-    double xr = tid < 12 ? sm[L::XIN + tid] : 0.0;
+    real* xo = sm + L::XO;
+    real xr = tid < 12 ? sm[L::XIN + tid] : 0.0;
     if (tid < 12) xo[tid] = xr;
-    const double qr = qdiag(tid_o);   // (not CSE-d with phase 2's copy)
+    const real qr = qdiag(tid_o);   // (not CSE-d with phase 2's copy)
     const int rw = (tid >= 9 && tid < 12) ? tid - 9 : 0;   // my row of Bd's omega block
     const int rv = (tid >= 6 && tid < 9) ? tid - 6 : 0;    // my row of Bd's velocity block
-    double objl = 0.0;
+    real objl = 0.0;
     sfor<0, N>([&](auto kc) __attribute__((always_inline)) {
       constexpr int k = decltype(kc)::value;
-      const double cp = sm[L::CS + 2 * k], sp = sm[L::CS + 2 * k + 1];
-      const double* bwr = sm + L::BW + 18 * k + 6 * rw;
-      const double* uk = xs + 6 * k;
-      double bw_u = 0.0;
+      const real cp = sm[L::CS + 2 * k], sp = sm[L::CS + 2 * k + 1];
+      const real* bwr = sm + L::BW + 18 * k + 6 * rw;
+      const real* uk = xs + 6 * k;
+      real bw_u = 0.0;
 #pragma unroll
       for (int c = 0; c < 6; ++c) bw_u = fma(bwr[c], uk[c], bw_u);
-      double bv_u = 0.0;
+      real bv_u = 0.0;
       if constexpr (VAR == 3) {
         bv_u = dtm2 * uk[rv];
       } else {   // Rz' dt/m
-        const double u0 = uk[0], u1 = uk[1], u2 = uk[2];
+        const real u0 = uk[0], u1 = uk[1], u2 = uk[2];
         bv_u = (rv == 0) ? dtm2 * (cp * u0 - sp * u1) : ((rv == 1) ? dtm2 * (sp * u0 + cp * u1) : dtm2 * u2);
       }
-      const double bu = (tid >= 9 && tid < 12) ? bw_u : ((tid >= 6 && tid < 9) ? bv_u : 0.0);
-      xr = ad_lane(xr, dt, cp, sp) + bu + ((tid == 8) ? -a.g * dt : 0.0);
-      const double kf = (k == N - 1) ? kTermQ : 1.0;
-      const double e = tid < 12 ? xr - xrg[k] : 0.0;
+      const real bu = (tid >= 9 && tid < 12) ? bw_u : ((tid >= 6 && tid < 9) ? bv_u : 0.0);
+      xr = ad_lane(xr, dt, cp, sp) + bu + ((tid == 8) ? -real(a.g) * dt : real(0));
+      const real kf = (k == N - 1) ? kTermQ : 1.0;
+      const real e = tid < 12 ? xr - xrg[k] : 0.0;
       objl = fma(kf * qr * e, e, objl);
       if (k < N - 1 && tid < 6) {   // (k is a constant here)
-        const double ub = a.uref_aliased ? ((sm[L::CC + N - 1] != 0.0) ? 2.0 * a.m * a.g : 0.0)
+        const real ub = a.uref_aliased ? ((sm[L::CC + N - 1] != 0.0) ? 2.0 * a.m * a.g : 0.0)
                                          : ((sm[L::CC + k] != 0.0) ? 2.0 * a.m * a.g : 0.0);
-        const double du = uk[tid] - (tid == 2 ? ub : 0.0);
-        objl = fma(kRdiag * du, du, objl);
+        const real du = uk[tid] - (tid == 2 ? ub : real(0));
+        objl = fma(real(kRdiag) * du, du, objl);
       }
       if (tid < 12) xo[12 * (k + 1) + tid] = xr;
     });
-    const double objv = B::sum(objl, red);
+    const real objv = B::sum(objl, red);
     __syncthreads();
 #ifndef HMPC_STAMPS
     if (a.x)
@@ -1390,6 +1417,8 @@ solve_kernel(SolveArgs a) {
   }
 }
 
+}  // namespace
+
 // ----------------------------------------------------------------------------
 // per-horizon launcher.  This file is compiled once per horizon with
 // -DHMPC_INST_N=<N> (see build.sh) so the instantiations build in parallel;
@@ -1401,16 +1430,20 @@ solve_kernel(SolveArgs a) {
 #define HMPC_CAT2(a, b) a##b
 #define HMPC_CAT(a, b) HMPC_CAT2(a, b)
 
-bool HMPC_CAT(launch_solve_n, HMPC_INST_N)(int variant, const SolveArgs& a, hipStream_t s) {
+#ifndef HMPC_LAUNCH_SUFFIX
+#define HMPC_LAUNCH_SUFFIX
+#endif
+bool HMPC_CAT(HMPC_CAT(launch_solve_n, HMPC_INST_N), HMPC_LAUNCH_SUFFIX)(int variant, const SolveArgs& a,
+                                                                     hipStream_t s) {
   constexpr int N = HMPC_INST_N;
   constexpr int NT = Lay<N>::NT;
   if (a.B <= 0) return true;
   if (variant == 3) {
-    hipLaunchKernelGGL((solve_kernel<3, N>), dim3((unsigned)a.B), dim3(NT), 0, s, a);
+    hipLaunchKernelGGL((solve_kernel<3, N, real>), dim3((unsigned)a.B), dim3(NT), 0, s, a);
     return true;
   }
   if (variant == 2) {
-    hipLaunchKernelGGL((solve_kernel<2, N>), dim3((unsigned)a.B), dim3(NT), 0, s, a);
+    hipLaunchKernelGGL((solve_kernel<2, N, real>), dim3((unsigned)a.B), dim3(NT), 0, s, a);
     return true;
   }
   return false;

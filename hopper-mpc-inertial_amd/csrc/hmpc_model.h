@@ -43,6 +43,10 @@ __device__ __forceinline__ double rsq_nr(double p) {
   const double e = fma(-(p * y), y, 1.0);
   return fma(y * e, fma(0.375, e, 0.5), y);
 }
+__device__ __forceinline__ float rsq_nr(float p) {   // fp32: v_rsq_f32 + one Newton step
+  const float y = __builtin_amdgcn_rsqf(p);
+  return y * fmaf(-0.5f * p * y, y, 1.5f);
+}
 
 // x of lane (r + D) within r's row of 16 lanes (D < 0: lane r - |D|); a DPP
 // row shift -- a VALU modifier, no LDS round trip like a bpermute.  Lanes

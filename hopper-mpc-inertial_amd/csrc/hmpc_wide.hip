@@ -770,7 +770,7 @@ bool launch_solve_wide(int variant, int N, const SolveArgs& a, hipStream_t s) {
   if (N < 1 || N > kWideNmax || !a.ws || a.ws_groups < 1) return false;
   if (a.B <= 0) return true;
   const int64_t g = a.B < a.ws_groups ? a.B : a.ws_groups;
-  const bool f32 = a.precision == 1;
+  const bool f32 = a.precision == 1 || a.precision == 5;
   if (variant == 3) {
     if (f32) hipLaunchKernelGGL((wide_kernel<3, float>), dim3((unsigned)g), dim3(WT), 0, s, a, N);
     else hipLaunchKernelGGL((wide_kernel<3, double>), dim3((unsigned)g), dim3(WT), 0, s, a, N);

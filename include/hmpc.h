@@ -67,13 +67,15 @@ extern "C" {
 
 /* arithmetic of the solve (hmpc_set_precision) */
 #define HMPC_PREC_F64 0           /* fp64; the dedicated kernel when N has one (default) */
-#define HMPC_PREC_F32 1           /* fp32 arithmetic (generic kernel; BASELINE configs[4]:
-                                     the tolerance/throughput trade-off)          */
+#define HMPC_PREC_F32 1           /* fp32 arithmetic (BASELINE configs[4]: the tolerance/
+                                     throughput trade-off): the dense kernel's fp32
+                                     build where N has one (N = 10), else generic */
 #define HMPC_PREC_F64_GENERIC 2   /* fp64 on the generic kernel (its fp32 twin's A/B) */
 #define HMPC_PREC_F64_RICCATI 3   /* fp64 on the Riccati kernel (any N <= 64; the default
                                      for 10 < N <= 64)                            */
 #define HMPC_PREC_F64_DENSE 4     /* fp64 on the dedicated dense kernel of N (compiled
                                      horizons only; the default for N <= 10)      */
+#define HMPC_PREC_F32_GENERIC 5   /* fp32 on the generic kernel (round-1 configs[4]) */
 
 typedef struct hmpc_ctx hmpc_ctx;
 

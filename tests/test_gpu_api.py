@@ -63,12 +63,15 @@ def test_bad_tensors_raise(hm):
 
 
 def test_kernel_names(hm):
-    assert make(hm, 10).kernel_name == 'hmpc::solve_kernel<3, 10>'
+    assert make(hm, 10).kernel_name == 'hmpc::solve_kernel<3, 10, double>'
     assert make(hm, 20).kernel_name == 'hmpc::ric_kernel<3, 2>'   # 2 waves / SIMD
     assert make(hm, 60).kernel_name == 'hmpc::ric_kernel<3, 1>'
     assert make(hm, 10, 'f64_riccati').kernel_name == 'hmpc::ric_kernel<3, 2>'
-    assert make(hm, 20, 'f64_dense').kernel_name == 'hmpc::solve_kernel<3, 20>'
+    assert make(hm, 20, 'f64_dense').kernel_name == 'hmpc::solve_kernel<3, 20, double>'
     assert make(hm, 10, 'f64_generic').kernel_name == 'hmpc::wide_kernel<3, double>'
+    assert make(hm, 10, 'f32').kernel_name == 'hmpc::solve_kernel<3, 10, float>'
+    assert make(hm, 20, 'f32').kernel_name == 'hmpc::wide_kernel<3, float>'   # no fp32 dense build
+    assert make(hm, 10, 'f32_generic').kernel_name == 'hmpc::wide_kernel<3, float>'
 
 
 def test_active_capacity(hm):

@@ -70,7 +70,7 @@ def solve_both(hm, N, inst, precision):
     return gpu, ref, kernel, cap
 
 
-@pytest.mark.parametrize('precision,kernel', [('f64', 'hmpc::solve_kernel<3, 10>'),
+@pytest.mark.parametrize('precision,kernel', [('f64', 'hmpc::solve_kernel<3, 10, double>'),
                                              ('f64_riccati', 'hmpc::ric_kernel<3, 2>')])
 def test_overflow_n10(hm, precision, kernel):
     N, B = 10, 48

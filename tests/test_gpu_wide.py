@@ -153,7 +153,8 @@ def test_generic_kernel_fp64_at_compiled_horizon(hm):
 
 
 def test_fp32_tradeoff_is_bounded_but_misses_the_tolerance(hm):
-    """BASELINE configs[4]: fp32 arithmetic (HMPC_PREC_F32).  Measured at
+    """BASELINE configs[4] on the generic kernel (HMPC_PREC_F32_GENERIC; the
+    dense kernel's fp32 build: test_gpu_f32.py).  Measured at
     B = 65536: every instance solved, max|du| = 1.07 N against the exact
     optimum (the reduced Hessian's condition ~3e6 eats fp32's 7 digits) and no
     throughput gain over the generic kernel's fp64 twin.  Pinned here: all
@@ -164,7 +165,8 @@ def test_fp32_tradeoff_is_bounded_but_misses_the_tolerance(hm):
     inst = hmpc_plan.sample_instances(B, N, curve=True, seed=78)
     c = ho.runner_constants()
     cx = hm.Context('3f', N, t=c['t'], m=c['m'], g=c['g'], mu=1.0, Jinv=c['Jinv'], rh=c['rh'],
-                    precision='f32')
+                    precision='f32_generic')
+    assert cx.kernel_name == 'hmpc::wide_kernel<3, float>'
     gpu = cx.solve_host(inst['x_in'], inst['x_lin'], inst['x_ref'], inst['pf'], inst['C'],
                         mu=inst['mu'])
     cx.close()
