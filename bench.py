@@ -39,6 +39,7 @@ sys.path.insert(0, ROOT)
 METRIC = 'QP solves/sec (N=10, 3f) at batch=65k, 1→8 MI355X; max |u*−u*_cvxpy|'
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level table)
 FP64_VECTOR_PEAK_TFS = 78.6   # MI355X FP64 vector (half the 157.3 TF FP32 vector rate)
+FP32_VECTOR_PEAK_TFS = 157.3  # MI355X FP32 vector (MI355X_MICROARCH.md)
 
 
 def algorithmic_bytes(N, with_mu=True):
@@ -303,8 +304,11 @@ def main():
         tj = json.load(open(tpath)).get(wl, {}) if os.path.exists(tpath) else {}
         if tj.get('kernel') == kernel:
             traffic = tj.get('bytes_per_launch_x2_corrected')
-            executed = tj.get('fp64_flops_executed_per_solve')
+            executed = None if 'float' in kernel else tj.get('fp64_flops_executed_per_solve')
         total = B * world * args.steps
+        f32 = 'float' in kernel
+        vec_key = 'fp32_vector' if f32 else 'fp64_vector'
+        vec_peak = FP32_VECTOR_PEAK_TFS if f32 else FP64_VECTOR_PEAK_TFS
         rec = {
             'metric': METRIC,
             'value': total / el,
@@ -333,9 +337,9 @@ def main():
                                          'FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md), null '
                                          'when no profile of this workload and kernel'},
             # the bound that matters for this path: fp64 VALU
-            'fp64_vector': {
-                'achieved': flops * B / (kern_ms * 1e-3) / 1e12, 'peak': FP64_VECTOR_PEAK_TFS,
-                'unit': 'TFLOP/s', 'frac': flops * B / (kern_ms * 1e-3) / 1e12 / FP64_VECTOR_PEAK_TFS,
+            vec_key: {
+                'achieved': flops * B / (kern_ms * 1e-3) / 1e12, 'peak': vec_peak,
+                'unit': 'TFLOP/s', 'frac': flops * B / (kern_ms * 1e-3) / 1e12 / vec_peak,
                 'flops_per_solve': flops, 'basis': 'algorithmic (bench.algorithmic_flops, DESIGN.md 5)',
                 'executed_flops_per_solve': executed},
             'cpu_baseline': base,
