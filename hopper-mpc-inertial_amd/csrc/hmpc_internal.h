@@ -39,8 +39,9 @@ struct SolveArgs {
   double* ws;
   int64_t ws_stride;   // in elements of the arithmetic type
   int ws_groups;
-  // 0: fp64 (dedicated kernel when the horizon has one), 1: fp32 generic
-  // kernel, 2: fp64 generic kernel, 3: fp64 Riccati kernel (HMPC_PREC_*)
+  // HMPC_PREC_*: 0 fp64 (fastest kernel for N), 1 fp32 (dense fp32 build
+  // where compiled, else generic), 2 fp64 generic, 3 fp64 Riccati, 4 fp64
+  // dense, 5 fp32 generic
   int precision;
   // Active-set overflow (hmpc_ric.hip): an instance whose active set outgrows
   // the LDS capacity of its kernel appends its index to ovf_list (count in
