@@ -41,6 +41,9 @@ struct hmpc_ctx {
   // Riccati kernel: per-workgroup K / G^-1 workspace of its resident grid
   double* kws = nullptr;
   int ric_groups = 0;
+  // planner scratch (footstep counter, peak lists)
+  void* plan_scratch = nullptr;
+  int64_t plan_scratch_bytes = 0;
   hipStream_t own_stream = nullptr;
 };
 
@@ -246,6 +249,7 @@ int hmpc_destroy(hmpc_ctx* c) {
   if (c->ovf) (void)hipFree(c->ovf);
   if (c->rws) (void)hipFree(c->rws);
   if (c->kws) (void)hipFree(c->kws);
+  if (c->plan_scratch) (void)hipFree(c->plan_scratch);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   delete c;
   return HMPC_OK;
@@ -524,6 +528,49 @@ int hmpc_convert_batch(hmpc_ctx* c, int64_t B, const double* X, double* x, void*
   if (!X || !x) { c->err = "null pointer"; return HMPC_ERR_ARG; }
   HMPC_HIP(c, hipSetDevice(c->device));
   hmpc::launch_convert(B, X, x, (hipStream_t)stream);
+  HMPC_HIP(c, hipGetLastError());
+  return HMPC_OK;
+}
+
+int hmpc_plan_batch(hmpc_ctx* c, int64_t B, int N_run, int N_k, double dt, int curve, double t_p,
+                    double phi_switch, double t_start, int step_adjustment, const double* x_in,
+                    const double* xf, double* x_ref, double* pf_ref, double* C_map, void* stream) {
+  if (!c) return HMPC_ERR_ARG;
+  if (B < 0 || N_run < 2 || N_k < 0 || !(dt > 0.0) || !(t_p > 0.0)) {
+    c->err = "B < 0, N_run < 2, N_k < 0, dt <= 0 or t_p <= 0";
+    return HMPC_ERR_ARG;
+  }
+  if (B == 0) return HMPC_OK;
+  if (!x_in || !xf || !x_ref || !pf_ref) { c->err = "null pointer"; return HMPC_ERR_ARG; }
+  HMPC_HIP(c, hipSetDevice(c->device));
+  const int64_t need = hmpc::plan_scratch_bytes(B, N_run + N_k);
+  if (need > c->plan_scratch_bytes) {
+    if (c->plan_scratch) (void)hipFree(c->plan_scratch);
+    c->plan_scratch = nullptr;
+    c->plan_scratch_bytes = 0;
+    hipError_t e = hipMalloc(&c->plan_scratch, (size_t)need);
+    if (e != hipSuccess) { c->err = "planner scratch hipMalloc"; return HMPC_ERR_NOMEM; }
+    c->plan_scratch_bytes = need;
+  }
+  hmpc::launch_plan(B, N_run, N_k, dt, curve, t_p, phi_switch, t_start, step_adjustment, x_in, xf, x_ref,
+                    pf_ref, C_map, c->plan_scratch, (hipStream_t)stream);
+  HMPC_HIP(c, hipGetLastError());
+  return HMPC_OK;
+}
+
+int hmpc_gait_batch(hmpc_ctx* c, int n_steps, int mpc_factor, int N, double dt, double mpc_dt, double t_p,
+                    double phi_switch, double t_start, double t0, double* C_calls, double* s_hist,
+                    void* stream) {
+  if (!c) return HMPC_ERR_ARG;
+  if (n_steps < 0 || mpc_factor < 1 || N < 1 || !(dt > 0.0) || !(mpc_dt > 0.0) || !(t_p > 0.0)) {
+    c->err = "n_steps < 0, mpc_factor < 1, N < 1 or a non-positive time";
+    return HMPC_ERR_ARG;
+  }
+  if (n_steps == 0) return HMPC_OK;
+  if (!C_calls) { c->err = "null pointer"; return HMPC_ERR_ARG; }
+  HMPC_HIP(c, hipSetDevice(c->device));
+  hmpc::launch_gait(n_steps, mpc_factor, N, dt, mpc_dt, t_p, phi_switch, t_start, t0, C_calls, s_hist,
+                    (hipStream_t)stream);
   HMPC_HIP(c, hipGetLastError());
   return HMPC_OK;
 }

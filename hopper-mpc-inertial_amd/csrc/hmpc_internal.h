@@ -145,6 +145,14 @@ struct PlantArgs {
 };
 void launch_plant(const PlantArgs& a, hipStream_t s);
 void launch_convert(int64_t B, const double* X, double* x, hipStream_t s);
+// the Runner's planner (hmpc_planner.hip)
+int64_t plan_scratch_bytes(int64_t B, int T);
+bool launch_plan(int64_t B, int N_run, int N_k, double dt, int curve, double t_p, double phi_switch,
+                 double t_start, int step_adjustment, const double* x_in, const double* xf, double* x_ref,
+                 double* pf_ref, double* C_map, void* scratch, hipStream_t s);
+bool launch_gait(int n_steps, int mpc_factor, int N, double dt, double mpc_dt, double t_p,
+                 double phi_switch, double t_start, double t0, double* C_calls, double* s_hist,
+                 hipStream_t s);
 
 // Which kernel solves (variant, N) at a precision (HMPC_PREC_*).
 enum class Kernel { None, Dense, DenseF32, Riccati, Wide };

@@ -45,6 +45,12 @@ SIGNATURES = {
                                         _VP, ctypes.c_int64, _VP, ctypes.c_int64, ctypes.c_int64,
                                         _VP, _VP, _VP]),
     'hmpc_convert_batch': (ctypes.c_int, [_VP, ctypes.c_int64, _VP, _VP, _VP]),
+    'hmpc_plan_batch': (ctypes.c_int, [_VP, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_double,
+                                       ctypes.c_int, ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                                       ctypes.c_int, _VP, _VP, _VP, _VP, _VP, _VP]),
+    'hmpc_gait_batch': (ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_double,
+                                       ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                                       ctypes.c_double, _VP, _VP, _VP]),
     'hmpc_set_precision': (ctypes.c_int, [_VP, ctypes.c_int]),
     'hmpc_last_error': (ctypes.c_char_p, [_VP]),
     'hmpc_kernel_name': (ctypes.c_char_p, [_VP]),
@@ -309,6 +315,46 @@ class Context:
                                         int(pf_sstride), _ptr(X_hist), _ptr(x_out),
                                         ctypes.c_void_p(s))
         self._check(rc, 'hmpc_plant_batch')
+
+    def plan_device(self, x_in, xf, N_run, N_k, dt, curve, t_p, phi_switch, t_start, step_adjustment,
+                    stream=None):
+        """Runner.path_plan_init (src/robotrunner.py:182-226) for B robots on
+        the device (hmpc_plan_batch): x_in / xf (B,12) start and goal states.
+        Returns x_ref (B,T,12), pf_ref (B,T,3) and the gait map C (T,),
+        T = N_run + N_k."""
+        import torch
+        B = x_in.shape[0]
+        _check_tensor(x_in, (B, 12), 'x_in', self.device)
+        _check_tensor(xf, (B, 12), 'xf', self.device)
+        T = int(N_run) + int(N_k)
+        dev = x_in.device
+        x_ref = torch.empty((B, T, 12), dtype=torch.float64, device=dev)
+        pf_ref = torch.empty((B, T, 3), dtype=torch.float64, device=dev)
+        C = torch.empty(T, dtype=torch.float64, device=dev)
+        s = stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
+        rc = self._lib.hmpc_plan_batch(self._h, B, int(N_run), int(N_k), float(dt), 1 if curve else 0,
+                                       float(t_p), float(phi_switch), float(t_start), int(step_adjustment),
+                                       _ptr(x_in), _ptr(xf), _ptr(x_ref), _ptr(pf_ref), _ptr(C),
+                                       ctypes.c_void_p(s))
+        self._check(rc, 'hmpc_plan_batch')
+        return x_ref, pf_ref, C
+
+    def gait_device(self, n_steps, mpc_factor, N, dt, mpc_dt, t_p, phi_switch, t_start, t0=0.0,
+                    device=None, stream=None):
+        """The Runner loop's gait schedule (hmpc_gait_batch): C_calls
+        (n_calls, N) = gait_map(N, mpc_dt, t_k, t0) at every MPC call and s_hist
+        (n_steps,) = gait_scheduler(t_k, t0) per low-level step."""
+        import torch
+        dev = torch.device('cuda', self.device) if device is None else device
+        n_calls = (int(n_steps) + int(mpc_factor) - 1) // int(mpc_factor)
+        C = torch.empty((n_calls, int(N)), dtype=torch.float64, device=dev)
+        s_hist = torch.empty(int(n_steps), dtype=torch.float64, device=dev)
+        s = stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
+        rc = self._lib.hmpc_gait_batch(self._h, int(n_steps), int(mpc_factor), int(N), float(dt),
+                                       float(mpc_dt), float(t_p), float(phi_switch), float(t_start),
+                                       float(t0), _ptr(C), _ptr(s_hist), ctypes.c_void_p(s))
+        self._check(rc, 'hmpc_gait_batch')
+        return C, s_hist
 
     def convert_device(self, X, x, stream=None):
         """x (B,12) = convert(X (B,13)) (src/robotrunner.py:19-28)."""

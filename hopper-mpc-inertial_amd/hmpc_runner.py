@@ -10,9 +10,11 @@ Per MPC period (mpc_factor low-level steps, src/robotrunner.py:92-113):
 * ``hmpc_plant_batch``          -- mpc_factor ``rk4_normalized`` steps with
   the first input row held (:109-111), then ``convert`` for the next solve.
 
-Host work per period is the gait schedule (``gait_map``, N numbers, the same
-float64 accumulation as the reference: src/robotrunner.py:166-180) and two
-kernel launches.  ``path_plan_init`` runs once on the host (hmpc_plan).
+The plan (``path_plan_init``, one per robot from its own start state, or one
+shared plan when all robots start alike) and the gait schedule (``gait_map``
+per MPC call, ``gait_scheduler`` per step) are made on the device too
+(``hmpc_plan_batch`` / ``hmpc_gait_batch``), so a period is two kernel
+launches and no host work.
 Plots are out of scope.
 
 There is no CPU fallback: without libhmpc.so or a GPU this raises.
@@ -48,6 +50,8 @@ class Runner:
                                 rh=self.rh, uref_mode=uref_mode, device=device)
         X0 = X0_DEFAULT if X0 is None else np.asarray(X0, dtype=np.float64)
         self.X0 = np.ascontiguousarray(np.broadcast_to(X0, (self.B, 13)))
+        # X_f = [dist, 0, 0.27, 1, 0 ...] (:58)
+        self.X_f = np.hstack([self.cfg.dist, 0, 0.27, 1, np.zeros(9)]).astype(np.float64)
 
     def close(self):
         self.ctx.close()
@@ -61,27 +65,31 @@ class Runner:
         import torch
         cfg, B, dev = self.cfg, self.B, self.device
         N, mf, dt = cfg.N, cfg.mpc_factor, cfg.dt
-        # plan (host, once): path_plan_init(convert(X_0), convert(X_f))  (:91)
-        x0, xf = hp.initial_states(cfg)
-        x_ref, pf_ref = hp.path_plan_init(cfg, x0, xf)
         steps = cfg.N_run if n_periods is None else min(cfg.N_run, int(n_periods) * mf)
-        # gait schedule per low-level step and per MPC call (float64 time
-        # accumulation exactly as the reference's loop, :96-101)
-        t = cfg.t_start
-        s_hist = np.zeros(steps)
-        call_k, C_rows = [], []
-        for k in range(steps):
-            t = t + dt
-            s_hist[k] = hp.gait_scheduler(cfg, t, 0)
-            if k % mf == 0:
-                call_k.append(k)
-                C_rows.append(hp.gait_map(cfg, N, cfg.mpc_dt, t, 0))
         f64 = dict(dtype=torch.float64, device=dev)
-        plan_x = torch.from_numpy(np.ascontiguousarray(x_ref)).to(dev)
-        plan_pf = torch.from_numpy(np.ascontiguousarray(pf_ref)).to(dev)
-        C_all = torch.from_numpy(np.ascontiguousarray(np.array(C_rows).reshape(-1, N))).to(dev)
         X = torch.from_numpy(self.X0.copy()).to(dev)
         x_in = torch.empty((B, 12), **f64)
+        self.ctx.convert_device(X, x_in)                                         # :102
+        # plan on the device: path_plan_init(convert(X_0), convert(X_f)) (:91),
+        # one plan per robot -- or one shared plan when every robot starts alike
+        shared = bool((self.X0 == self.X0[:1]).all())
+        Bp = 1 if shared else B
+        Xf = torch.from_numpy(np.tile(self.X_f, (Bp, 1))).to(dev)
+        xf = torch.empty((Bp, 12), **f64)
+        self.ctx.convert_device(Xf, xf)
+        x0p = x_in[:1].clone() if shared else x_in.clone()
+        plan_x, plan_pf, _ = self.ctx.plan_device(x0p, xf, cfg.N_run, cfg.N_k, dt, cfg.curve, cfg.t_p,
+                                                  cfg.phi_switch, cfg.t_start, cfg.step_adjustment)
+        T = plan_x.shape[1]
+        if shared:
+            plan_x, plan_pf = plan_x[0], plan_pf[0]
+        # gait schedule per low-level step and per MPC call, on the device
+        # (the reference's float64 time accumulation, :92-101)
+        C_all, s_hist_d = self.ctx.gait_device(steps, mf, N, dt, cfg.mpc_dt, cfg.t_p, cfg.phi_switch,
+                                               cfg.t_start, 0.0)
+        call_k = list(range(0, steps, mf))
+        pf_flat = plan_pf.reshape(-1)
+        pf_bs = 0 if shared else 3 * T
         x_prev = torch.zeros((B, N + 1, 12), **f64)
         out = dict(u=torch.empty((B, N, 6), **f64), obj=torch.empty(B, **f64),
                    status=torch.empty(B, dtype=torch.int32, device=dev),
@@ -92,13 +100,12 @@ class Runner:
         if record:
             X_traj[:, 0] = X
         status = torch.empty((len(call_k), B), dtype=torch.int32, device=dev)
-        self.ctx.convert_device(X, x_in)                                         # :102
         for p, k in enumerate(call_k):
             self.ctx.mpcontrol_plan_device(p == 0, x_in, plan_x, plan_pf, k, mf, C_all[p], x_prev,
                                            out=out)                             # :98-103
             status[p] = out['status']
             n = min(mf, steps - k)
-            self.ctx.plant_device(X, out['u'], 6 * N, plan_pf[k:], 0, 3, n, dt, self.J,
+            self.ctx.plant_device(X, out['u'], 6 * N, pf_flat[3 * k:], pf_bs, 3, n, dt, self.J,
                                   X_hist=hist if record else None, x_out=x_in)   # :109-111
             if record:
                 X_traj[:, k + 1:k + 1 + n] = hist[:, :n]
@@ -109,8 +116,8 @@ class Runner:
             bad = np.argwhere(st != 0)[0]
             raise Exception(f"\n *** QP FAILED *** \n (call {bad[0]}, robot {bad[1]}: "
                             f"{hmpc.STATUS.get(int(st[bad[0], bad[1]]), st[bad[0], bad[1]])})")
-        res = dict(X_final=X.cpu().numpy(), s_hist=s_hist, status=st, x_ref=x_ref, pf_ref=pf_ref,
-                   call_k=np.array(call_k))
+        res = dict(X_final=X.cpu().numpy(), s_hist=s_hist_d.cpu().numpy(), status=st,
+                   x_ref=plan_x.cpu().numpy(), pf_ref=plan_pf.cpu().numpy(), call_k=np.array(call_k))
         if record:
             res['X_traj'] = X_traj.cpu().numpy()
             res['f_hist'] = f_hist.cpu().numpy()

@@ -24,6 +24,10 @@
  *                           (src/robotrunner.py:126-164) for n_steps
  *                           low-level steps, then convert (:19-28)
  *   hmpc_convert_batch   <- convert(X) (src/robotrunner.py:19-28)
+ *   hmpc_plan_batch      <- Runner.path_plan_init (src/robotrunner.py:182-226)
+ *                           + gait_map (:174-180), one plan per robot
+ *   hmpc_gait_batch      <- the Runner loop's gait_scheduler / gait_map calls
+ *                           (src/robotrunner.py:92-101)
  *   hmpc_destroy         <- object lifetime
  *
  * Conventions: every array is row-major, contiguous, float64, batch-major
@@ -171,6 +175,27 @@ int hmpc_plant_batch(hmpc_ctx* ctx, int64_t B, int n_steps, double dt, const dou
 
 /* x [B,12] = convert(X [B,13]) (src/robotrunner.py:19-28).  Asynchronous. */
 int hmpc_convert_batch(hmpc_ctx* ctx, int64_t B, const double* X, double* x, void* stream);
+
+/* Runner.path_plan_init (src/robotrunner.py:182-226) for B robots on the
+   device: robot b's plan from its own start x_in[b] and goal xf[b] (convert()ed
+   MPC states, [B,12] device) into x_ref [B,T,12] and pf_ref [B,T,3], T = N_run +
+   N_k (N_k = N * mpc_factor: the MPC horizon in low-level steps).  curve != 0 is
+   the --curve plan with the reference's quirks (:193-201).  t_p, phi_switch,
+   t_start and step_adjustment are the Runner's gait constants (:44-49,78-79);
+   C_map [T] (optional) receives gait_map(T, dt, t_start, 0) (:213).  Feeds
+   hmpc_mpcontrol_plan_batch with plan_bstride = T.  Asynchronous. */
+int hmpc_plan_batch(hmpc_ctx* ctx, int64_t B, int N_run, int N_k, double dt, int curve, double t_p,
+                    double phi_switch, double t_start, int step_adjustment, const double* x_in,
+                    const double* xf, double* x_ref, double* pf_ref, double* C_map, void* stream);
+
+/* The Runner loop's gait schedule (src/robotrunner.py:92-101,166-180) on the
+   device: t = t_start; for step k < n_steps: t += dt, s_hist[k] =
+   gait_scheduler(t, t0) (optional output), and at every MPC call (k % mpc_factor
+   == 0) the row C_calls[p] = gait_map(N, mpc_dt, t, t0) of [n_calls, N], with
+   the reference's float64 time accumulation.  Asynchronous. */
+int hmpc_gait_batch(hmpc_ctx* ctx, int n_steps, int mpc_factor, int N, double dt, double mpc_dt, double t_p,
+                    double phi_switch, double t_start, double t0, double* C_calls, double* s_hist,
+                    void* stream);
 
 /* Arithmetic of every later solve on this context (HMPC_PREC_*; inputs and
    outputs stay fp64 at the ABI).  BASELINE configs[4] asks for fp32 vs fp64:

@@ -122,11 +122,13 @@ def run_closed_loop(N=10, N_run=1000, curve=False, variant='3f', n_periods=None,
     c = ho.runner_constants()
     J = c['J']
     mpc = ho.OracleMpc(ho.MpcParams.runner(variant, N))
-    x0, xf = hp.initial_states(cfg)
-    x_ref, pf_ref = hp.path_plan_init(cfg, x0, xf)
     X_traj = np.tile(np.array([0, 0, 0.27, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0], float), (N_run + 1, 1))
     if X0 is not None:
         X_traj[0] = X0
+    # the plan from the robot's own start (src/robotrunner.py:91):
+    # path_plan_init(convert(X_traj[0]), convert(X_f)), X_f = [dist, 0, 0.27, 1, 0...] (:58)
+    X_f = np.hstack([cfg.dist, 0, 0.27, 1, np.zeros(9)])
+    x_ref, pf_ref = hp.path_plan_init(cfg, convert(X_traj[0]), convert(X_f))
     f_hist = np.zeros((N_run, 6))
     t = cfg.t_start
     mf = cfg.mpc_factor
