@@ -38,6 +38,8 @@ $HIPCC $FLAGS -c csrc/hmpc_plant.hip -o $BDIR/hmpc_plant.o &
 pids+=($!)
 $HIPCC $FLAGS -c csrc/hmpc_planner.hip -o $BDIR/hmpc_planner.o &
 pids+=($!)
+$HIPCC $FLAGS -c csrc/hmpc_cas.hip -o $BDIR/hmpc_cas.o "$@" &
+pids+=($!)
 $HIPCC $FLAGS -c csrc/hmpc_wide.hip -o $BDIR/hmpc_wide.o "$@" &
 pids+=($!)
 $HIPCC $FLAGS -c csrc/hmpc_ric.hip -o $BDIR/hmpc_ric.o "$@" &
@@ -46,6 +48,6 @@ for p in "${pids[@]}"; do wait "$p"; done
 objs=""
 for n in $HORIZONS; do objs="$objs $BDIR/hmpc_kernels_n$n.o"; done
 for n in $F32_HORIZONS; do objs="$objs $BDIR/hmpc_kernels_n${n}_f32.o"; done
-$HIPCC --offload-arch=gfx950 -shared -fPIC $objs $BDIR/hmpc_dispatch.o $BDIR/hmpc_capi.o $BDIR/hmpc_plant.o $BDIR/hmpc_planner.o $BDIR/hmpc_wide.o $BDIR/hmpc_ric.o -o $OUT.tmp
+$HIPCC --offload-arch=gfx950 -shared -fPIC $objs $BDIR/hmpc_dispatch.o $BDIR/hmpc_capi.o $BDIR/hmpc_plant.o $BDIR/hmpc_planner.o $BDIR/hmpc_cas.o $BDIR/hmpc_wide.o $BDIR/hmpc_ric.o -o $OUT.tmp
 mv $OUT.tmp $OUT
 echo "built $(pwd)/$OUT (horizons: $HORIZONS)"

@@ -126,6 +126,25 @@ int prepare_ric(hmpc_ctx* c, int64_t B, hmpc::SolveArgs& a) {
   const hmpc::Kernel k = hmpc::pick_kernel(c->variant, c->N, c->precision);
   a.ovf_count = nullptr; a.ovf_list = nullptr; a.rws = nullptr; a.rws_stride = 0;
   a.work = nullptr; a.kws = nullptr; a.kws_stride = 0; a.ric_groups = 0;
+  if (k == hmpc::Kernel::Cas) {   // instance counter + R slots, no overflow pass
+    if (!c->ovf) {
+      hipError_t e = hipMalloc(&c->ovf, sizeof(int32_t) * 4);
+      if (e != hipSuccess) { c->err = "counter hipMalloc"; return HMPC_ERR_NOMEM; }
+      c->ovf_cap = 0;
+    }
+    if (c->ric_groups == 0) {
+      const int g = hmpc::cas_groups(c->N);
+      if (g < 1) { c->err = "CasADi-variant kernel occupancy query"; return HMPC_ERR_HIP; }
+      hipError_t e = hipMalloc(&c->kws, sizeof(double) * hmpc::cas_ws_stride(c->N) * g);
+      if (e != hipSuccess) { c->kws = nullptr; c->err = "CasADi-variant workspace hipMalloc"; return HMPC_ERR_NOMEM; }
+      c->ric_groups = g;
+    }
+    a.work = c->ovf + 1;
+    a.kws = c->kws;
+    a.kws_stride = hmpc::cas_ws_stride(c->N);
+    a.ric_groups = c->ric_groups;
+    return HMPC_OK;
+  }
   // (the fp32 dense build hands its overflows to the same fp64 pass)
   if ((k != hmpc::Kernel::Dense && k != hmpc::Kernel::DenseF32 && k != hmpc::Kernel::Riccati) ||
       c->N > hmpc::kRicNmax)
@@ -170,8 +189,8 @@ int run_solve(hmpc_ctx* c, hmpc::SolveArgs a, hipStream_t s) {
   if (rc != HMPC_OK) return rc;
   rc = prepare_ric(c, a.B, a);
   if (rc != HMPC_OK) return rc;
-  if (a.ovf_count) {   // overflow count and instance counter
-    hipError_t e = hipMemsetAsync(a.ovf_count, 0, 2 * sizeof(int32_t), s);
+  if (a.ovf_count || a.work) {   // overflow count and instance counter
+    hipError_t e = hipMemsetAsync(a.ovf_count ? a.ovf_count : a.work - 1, 0, 2 * sizeof(int32_t), s);
     if (e != hipSuccess) return fail_hip(c, e, "hipMemsetAsync(overflow count)");
   }
   if (!hmpc::launch_solve(c->variant, c->N, a, s)) {
@@ -223,7 +242,7 @@ int hmpc_create(hmpc_ctx** out, int variant, int N, double t, double m, double g
                 const double* Jinv, const double* rh, int uref_mode, int device) {
   if (!out || !Jinv || !rh) return HMPC_ERR_ARG;
   *out = nullptr;
-  if (variant != HMPC_VARIANT_3F && variant != HMPC_VARIANT_2F) return HMPC_ERR_ARG;
+  if (variant != HMPC_VARIANT_3F && variant != HMPC_VARIANT_2F && variant != HMPC_VARIANT_CAS) return HMPC_ERR_ARG;
   if (uref_mode != HMPC_UREF_ALIASED && uref_mode != HMPC_UREF_PER_STAGE) return HMPC_ERR_ARG;
   if (!(t > 0.0) || !(m > 0.0) || N <= 0) return HMPC_ERR_ARG;
   if (!hmpc::horizon_supported(variant, N)) return HMPC_ERR_UNSUPPORTED;
@@ -267,6 +286,8 @@ int hmpc_active_capacity(hmpc_ctx* c) {
     }
     case hmpc::Kernel::Riccati:
       return hmpc::ric_qcap(c->N);
+    case hmpc::Kernel::Cas:
+      return 18 * c->N;
     case hmpc::Kernel::Wide:
       return 0;
     default:
@@ -287,6 +308,8 @@ const char* hmpc_kernel_name(hmpc_ctx* c) {
     }
     case hmpc::Kernel::DenseF32:
       return v3 ? "hmpc::solve_kernel<3, 10, float>" : "hmpc::solve_kernel<2, 10, float>";
+    case hmpc::Kernel::Cas:
+      return "hmpc::cas_kernel";
     case hmpc::Kernel::Riccati:
       if (hmpc::ric_occ(c->N) == 2) return v3 ? "hmpc::ric_kernel<3, 2>" : "hmpc::ric_kernel<2, 2>";
       return v3 ? "hmpc::ric_kernel<3, 1>" : "hmpc::ric_kernel<2, 1>";

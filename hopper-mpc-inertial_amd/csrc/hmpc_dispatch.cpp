@@ -42,6 +42,7 @@ bool horizon_compiled(int variant, int N) {
 }
 
 Kernel pick_kernel(int variant, int N, int precision) {
+  if (variant == 4) return (precision == 0 && N >= 1 && N <= kCasNmax) ? Kernel::Cas : Kernel::None;
   if (variant != 2 && variant != 3 || N < 1) return Kernel::None;
   switch (precision) {
     case 1:
@@ -84,12 +85,15 @@ bool launch_solve(int variant, int N, const SolveArgs& a, hipStream_t s) {
       return launch_solve_ric(variant, N, a, s);
     case Kernel::Wide:
       return launch_solve_wide(variant, N, a, s);
+    case Kernel::Cas:
+      return launch_solve_cas(N, a, s);
     default:
       return false;
   }
 }
 
 bool horizon_supported(int variant, int N) {
+  if (variant == 4) return N >= 1 && N <= kCasNmax;
   if (variant != 2 && variant != 3) return false;
   return horizon_compiled(variant, N) || (N >= 1 && N <= kWideNmax);
 }

@@ -145,6 +145,14 @@ struct PlantArgs {
 };
 void launch_plant(const PlantArgs& a, hipStream_t s);
 void launch_convert(int64_t B, const double* X, double* x, hipStream_t s);
+// the CasADi variant's kernel (hmpc_cas.hip): R slots of cas_ws_stride
+// doubles per resident workgroup in a.kws, instance counter a.work,
+// a.ric_groups workgroups
+constexpr int kCasNmax = 11;
+size_t cas_lds_bytes(int N);
+int64_t cas_ws_stride(int N);
+int cas_groups(int N);
+bool launch_solve_cas(int N, const SolveArgs& a, hipStream_t s);
 // the Runner's planner (hmpc_planner.hip)
 int64_t plan_scratch_bytes(int64_t B, int T);
 bool launch_plan(int64_t B, int N_run, int N_k, double dt, int curve, double t_p, double phi_switch,
@@ -155,7 +163,7 @@ bool launch_gait(int n_steps, int mpc_factor, int N, double dt, double mpc_dt, d
                  hipStream_t s);
 
 // Which kernel solves (variant, N) at a precision (HMPC_PREC_*).
-enum class Kernel { None, Dense, DenseF32, Riccati, Wide };
+enum class Kernel { None, Dense, DenseF32, Riccati, Wide, Cas };
 Kernel pick_kernel(int variant, int N, int precision);
 // Launch the solve kernel for (variant, N, a.precision).  Returns false when
 // no kernel serves that combination.  Dense and Riccati kernels honour

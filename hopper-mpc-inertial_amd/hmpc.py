@@ -19,7 +19,7 @@ LIB_PATH = os.environ.get('HMPC_LIB', os.path.join(HERE, 'libhmpc.so'))
 HMPC_OK = 0
 ERRORS = {-1: 'HMPC_ERR_ARG', -2: 'HMPC_ERR_UNSUPPORTED', -3: 'HMPC_ERR_HIP', -4: 'HMPC_ERR_NOMEM'}
 STATUS = {0: 'solved', 1: 'max_iter', 2: 'primal_infeasible', 3: 'numerical'}
-VARIANTS = {'3f': 3, '2f': 2, 3: 3, 2: 2}
+VARIANTS = {'3f': 3, '2f': 2, 'cas': 4, 3: 3, 2: 2, 4: 4}
 UREF = {'aliased': 0, 'per_stage': 1}
 PRECISION = {'f64': 0, 'f32': 1, 'f64_generic': 2, 'f64_riccati': 3, 'f64_dense': 4, 'f32_generic': 5}
 

@@ -63,6 +63,12 @@ extern "C" {
 /* variants: the two dynamics formulations of the reference */
 #define HMPC_VARIANT_3F 3         /* src/mpc_cvx_euler_3f.py: world-frame force */
 #define HMPC_VARIANT_2F 2         /* src/mpc_cvx_euler_2f.py: body-frame, fy = 0 */
+#define HMPC_VARIANT_CAS 4        /* src/mpc_cas_euler_3f.py: the CasADi/qpOASES
+                                     variant's QP as the reference builds it
+                                     (second-order discretisation at the yaw of
+                                     x_in, one-sided dynamics rows, scalar u_ref;
+                                     x_lin and pf are ignored, rf is fixed);
+                                     1 <= N <= 11, fp64 only */
 
 /* u_ref semantics */
 #define HMPC_UREF_ALIASED 0       /* what cvxpy actually solves: every stage sees

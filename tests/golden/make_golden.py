@@ -18,7 +18,11 @@ What it does:
   solution carries its KKT certificate;
 * planner: ``Runner.path_plan_init`` (straight and --curve), ``gait_map``;
 * closed loop: the reference Runner loop (gait, plan grab, convert,
-  ``Mpc.mpcontrol``, ``rk4_normalized``) at N=10 and, for config 1, N=60.
+  ``Mpc.mpcontrol``, ``rk4_normalized``) at N=10 and, for config 1, N=60;
+* the CasADi variant (src/mpc_cas_euler_3f.py): its own Mpc builds its QP
+  through a recording casadi stub (tests/golden/_stubs/casadi, sympy
+  algebra); the QP data handed to qpOASES is recorded and solved exactly by
+  oracle/cas_oracle.py (qpOASES is absent: solve parity unpinned).
 
 Only inputs and outputs are written (npz); no reference source is copied.
 """
@@ -228,6 +232,48 @@ def make_closed_loop_fixture(N, N_run, curve, name, n_detail):
     print(f'{name}: {ncall} mpcontrol calls')
 
 
+def make_cas_fixture(N, B, seed, curve=True):
+    """The CasADi variant's QP data (src/mpc_cas_euler_3f.py:14-152) for B
+    sampled instances, as the reference's own Mpc builds it."""
+    import casadi  # noqa: F401  (the recording stub)
+    import mpc_cas_euler_3f as refcas
+    from oracle import cas_oracle
+    casadi.SOLVER = lambda rec: cas_oracle.solve(rec, N)['z']
+    rr, plan, pf_plan = reference_plan(curve)
+    rng = np.random.default_rng(seed)
+    insts = sample(rr, plan, pf_plan, B, N, rng)
+    mpc = refcas.Mpc(t=rr.mpc_dt, N=N, Jinv=rr.Jinv, rh=rr.rh, m=rr.m, g=rr.g, mu=1)
+    keys = ('x_in', 'x_ref', 'C', 'Pdiag', 'q', 'r', 'g0', 'lbg', 'ubg', 'lbx', 'ubx', 'u', 'z')
+    arrs = {k: [] for k in keys}
+    A_r, A_c, A_v, A_n = [], [], [], []
+    for inst in insts:
+        n0 = len(casadi.RECORD)
+        u = mpc.mpcontrol(x_in=inst['x_in'], x_ref_in=inst['x_ref'], rf=inst['pf'], C=inst['C'])
+        rec = casadi.RECORD[n0]
+        P = rec['P']
+        assert np.count_nonzero(P - np.diag(np.diag(P))) == 0
+        vals = dict(x_in=inst['x_in'], x_ref=inst['x_ref'], C=inst['C'], Pdiag=np.diag(P), q=rec['q'],
+                    r=rec['r'], g0=rec['g0'], lbg=rec['lbg'], ubg=rec['ubg'], lbx=rec['lbx'],
+                    ubx=rec['ubx'], u=u, z=rec['z'])
+        for k in keys:
+            arrs[k].append(vals[k])
+        r, c, v = coo(rec['A'])
+        A_r.append(r); A_c.append(c); A_v.append(v); A_n.append(len(v))
+    out = {k: np.array(v) for k, v in arrs.items()}
+    out['A_row'] = np.concatenate(A_r)
+    out['A_col'] = np.concatenate(A_c)
+    out['A_val'] = np.concatenate(A_v)
+    out['A_nnz'] = np.array(A_n)
+    out['A_shape'] = np.array(rec['A'].shape)
+    out['N'] = np.array(N)
+    out['curve'] = np.array(curve)
+    out['Jinv'] = rr.Jinv
+    out['rh'] = rr.rh
+    name = f'cas_N{N}.npz'
+    np.savez_compressed(os.path.join(HERE, name), **out)
+    print(f'{name}: {B} instances, A {rec["A"].shape}')
+
+
 def make_plant_fixture():
     """dynamics_ct / rk4_normalized / convert samples."""
     rr = robotrunner.Runner(dt=1e-3, dyn='3f', curve=False, N_run=2000)
@@ -244,7 +290,7 @@ def make_plant_fixture():
 
 
 if __name__ == '__main__':
-    which = sys.argv[1:] or ['plan', 'qp', 'loop', 'plant']
+    which = sys.argv[1:] or ['plan', 'qp', 'loop', 'plant', 'cas']
     if 'plan' in which:
         make_plan_fixture()
     if 'plant' in which:
@@ -256,6 +302,8 @@ if __name__ == '__main__':
         make_qp_fixture('2f', 10, True, 16, 4, seed=4)
         make_qp_fixture('3f', 20, False, 12, 3, seed=5, mu_sweep=(0.3, 1.2))
         make_qp_fixture('3f', 10, True, 16, 2, seed=6, mu_sweep=(0.3, 1.2))
+    if 'cas' in which:
+        make_cas_fixture(10, 8, seed=21)
     if 'loop' in which:
         make_closed_loop_fixture(10, 1000, False, 'loop_3f_N10.npz', n_detail=50)
         make_closed_loop_fixture(60, 2000, False, 'loop_3f_N60_config1.npz', n_detail=100)

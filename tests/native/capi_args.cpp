@@ -29,7 +29,8 @@ int main() {
   EXPECT(hmpc_create(nullptr, 3, 10, 0.02, 7.5, 9.807, 1.0, Jinv, rh, 0, 0) == HMPC_ERR_ARG);
   EXPECT(hmpc_create(&c, 3, 10, 0.02, 7.5, 9.807, 1.0, nullptr, rh, 0, 0) == HMPC_ERR_ARG);
   EXPECT(hmpc_create(&c, 3, 10, 0.02, 7.5, 9.807, 1.0, Jinv, nullptr, 0, 0) == HMPC_ERR_ARG);
-  EXPECT(hmpc_create(&c, 4, 10, 0.02, 7.5, 9.807, 1.0, Jinv, rh, 0, 0) == HMPC_ERR_ARG);
+  EXPECT(hmpc_create(&c, 5, 10, 0.02, 7.5, 9.807, 1.0, Jinv, rh, 0, 0) == HMPC_ERR_ARG);
+  EXPECT(hmpc_create(&c, 4, 12, 0.02, 7.5, 9.807, 1.0, Jinv, rh, 0, 0) == HMPC_ERR_UNSUPPORTED);   // CasADi variant: N <= 11
   EXPECT(hmpc_create(&c, 3, 0, 0.02, 7.5, 9.807, 1.0, Jinv, rh, 0, 0) == HMPC_ERR_ARG);
   EXPECT(hmpc_create(&c, 3, 10, 0.0, 7.5, 9.807, 1.0, Jinv, rh, 0, 0) == HMPC_ERR_ARG);
   EXPECT(hmpc_create(&c, 3, 10, 0.02, -1.0, 9.807, 1.0, Jinv, rh, 0, 0) == HMPC_ERR_ARG);

@@ -41,7 +41,7 @@ def test_port_under_asan_ubsan():
 def test_capi_argument_checks_under_asan_ubsan(tmp_path):
     pkg = os.path.join(ROOT, 'hopper-mpc-inertial_amd')
     objs = [os.path.join(pkg, 'build', f) for f in
-            ('hmpc_kernels_n5.o', 'hmpc_kernels_n10.o', 'hmpc_kernels_n20.o', 'hmpc_kernels_n10_f32.o', 'hmpc_plant.o', 'hmpc_planner.o',
+            ('hmpc_kernels_n5.o', 'hmpc_kernels_n10.o', 'hmpc_kernels_n20.o', 'hmpc_kernels_n10_f32.o', 'hmpc_plant.o', 'hmpc_planner.o', 'hmpc_cas.o',
              'hmpc_wide.o', 'hmpc_ric.o')]
     if not all(os.path.exists(o) for o in objs):
         subprocess.check_call(['bash', os.path.join(pkg, 'build.sh')])
