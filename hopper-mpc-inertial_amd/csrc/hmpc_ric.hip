@@ -150,9 +150,13 @@ __device__ __forceinline__ void vset(double (&v)[ENT], int i, double x) {
   for (int e = 0; e < ENT; ++e) v[e] = (64 * e + lane == i) ? x : v[e];
 }
 
-template <int VAR, int ENT, int RING>
+constexpr double kZcRel = 1e-3;
+// ZC: z = H^-1 (n_p - N_A r) as s - sum_a r_a S_a from the cached columns
+// S_a = H^-1 n_a of the active rows (scw: cap x NV, kept in active order),
+// instead of a third pair of sweeps per iteration
+template <int VAR, int ENT, int RING, bool ZC>
 __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, double* sm, double* Rm,
-                          const int cap, double* kw) {
+                          const int cap, double* kw, double* scw) {
   // lane and N through volatile asm: made afresh for every instance, so the
   // compiler cannot hoist lane- and N-derived values (masks, offsets) out of
   // the persistent instance loop and hold them -- spilled -- for the kernel's
@@ -919,15 +923,40 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
           for (int c = 0; c < 6; ++c) nb[6 * j + c] = acc[c];
         }
         rsync();
-        int tz = stage_top(p);   // n_p - N_A r: the last stage of p and the active rows
-#pragma unroll
-        for (int e = 0; e < ENT; ++e) {
-          const int ai = 64 * e + lane;
-          if (ai < q) tz = max(tz, stage_top(act[ai]));
+        bool sweep = !ZC;
+        if constexpr (ZC) {
+          for (int i = lane; i < NV; i += RT) {
+            const double* sc = scw + i;
+            double z0 = sv[i], z1 = 0.0;
+            int a0 = 0;
+            for (; a0 + 4 <= q; a0 += 4) {
+              const double c0 = sc[(int64_t)a0 * NV], c1 = sc[(int64_t)(a0 + 1) * NV];
+              const double c2 = sc[(int64_t)(a0 + 2) * NV], c3 = sc[(int64_t)(a0 + 3) * NV];
+              z0 = fma(-cbv[a0], c0, z0);
+              z1 = fma(-cbv[a0 + 1], c1, z1);
+              z0 = fma(-cbv[a0 + 2], c2, z0);
+              z1 = fma(-cbv[a0 + 3], c3, z1);
+            }
+            for (; a0 < q; ++a0) z0 = fma(-cbv[a0], sc[(int64_t)a0 * NV], z0);
+            zv[i] = z0 + z1;
+          }
+          rsync();
+          // the cached form cancels in H^-1 space: when n_z'z is small against
+          // n_p'H^-1 n_p the result is recomputed by the sweeps
+          zn = vdot(nb, zv);
+          sweep = !(zn > kZcRel * sn);
         }
-        hinv(zv, wave_imax63(tz));
+        if (sweep) {
+          int tz = stage_top(p);   // n_p - N_A r: the last stage of p and the active rows
+#pragma unroll
+          for (int e = 0; e < ENT; ++e) {
+            const int ai = 64 * e + lane;
+            if (ai < q) tz = max(tz, stage_top(act[ai]));
+          }
+          hinv(zv, wave_imax63(tz));
+          zn = vdot(nb, zv);
+        }
         zsrc = zv;
-        zn = vdot(nb, zv);
       }
       RS_ACC(7, t_z);
       RS_T(t_u);
@@ -973,6 +1002,8 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
           ua[q] = uplus;
         }
         if (lane == (p >> 2) / 6) amask |= 1 << (4 * ((p >> 2) % 6) + (p & 3));
+        if constexpr (ZC)   // cache S_q = H^-1 n_p (each lane its own entries)
+          for (int i = lane; i < NV; i += RT) scw[(int64_t)q * NV + i] = sv[i];
         ++q;
         rsync();
         RS_ACC(8, t_u);
@@ -983,6 +1014,9 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
         const int k = uni(kdrop);
         const int idk = act[k];
         if (lane == (idk >> 2) / 6) amask &= ~(1 << (4 * ((idk >> 2) % 6) + (idk & 3)));
+        if constexpr (ZC)   // the cached columns follow the active order
+          for (int m = k; m + 1 < q; ++m)
+            for (int i = lane; i < NV; i += RT) scw[(int64_t)m * NV + i] = scw[(int64_t)(m + 1) * NV + i];
         for (int m = k; m + 1 < q; ++m) {   // shift columns m+1 -> m, keep subdiagonals
           for (int i0 = 0; i0 <= m + 1; i0 += RT) {
             const int i = i0 + lane;
@@ -1114,7 +1148,8 @@ __global__ void __launch_bounds__(RT) __attribute__((amdgpu_waves_per_eu(OCC, OC
     if (threadIdx.x == 0) b = atomicAdd(a.work, 1);
     b = __builtin_amdgcn_readfirstlane(b);
     if (b >= a.B) break;
-    ric_solve<VAR, 1, OCC == 2 ? 2 : 3>(a, N, (int64_t)b, ric_sm, ric_sm + L.RM, cap, kw);
+    ric_solve<VAR, 1, OCC == 2 ? 2 : 3, true>(a, N, (int64_t)b, ric_sm, ric_sm + L.RM, cap, kw,
+                                              kw + ric_kws_doubles(N));
     __syncthreads();
   }
 }
@@ -1131,7 +1166,7 @@ __global__ void __launch_bounds__(RT) ric_overflow_kernel(SolveArgs a, int N) {
   a2.ovf_count = nullptr;   // no further overflow: capacity is 6N
   for (int i = blockIdx.x; i < n; i += gridDim.x) {
     const int64_t b = a.ovf_list[i];
-    ric_solve<VAR, (6 * kRicNmax + 63) / 64, 3>(a2, N, b, ric_sm, Rm, 6 * N, kw);
+    ric_solve<VAR, (6 * kRicNmax + 63) / 64, 3, false>(a2, N, b, ric_sm, Rm, 6 * N, kw, nullptr);
     __syncthreads();
   }
 }
@@ -1169,7 +1204,10 @@ RicCfg ric_config(int N) {
 int ric_qcap(int N) { return ric_config(N).cap; }
 int ric_occ(int N) { return ric_config(N).occ; }
 
-int64_t ric_kws_stride(int N) { return ric_kws_doubles(N); }
+// K / G^-1 of every stage, then the cached columns H^-1 n_a (capacity x NV)
+int64_t ric_kws_stride(int N) {
+  return ric_kws_doubles(N) + ((((int64_t)ric_qcap(N) * 6 * N) + 15) & ~(int64_t)15);
+}
 
 int64_t ric_rws_stride(int N) {
   const int64_t nv = 6 * (int64_t)N;
