@@ -284,7 +284,8 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
     double* T = un + TS_OFF;    // P B, 12 x 6
     double* F = un + FS_OFF;    // B'P A, 6 x 12
     double* G = un + GS_OFF;    // 6 x 6
-    double* Dl = un + DL_OFF;   // Dinv, packed lower
+    // F[c][j]: stored for j >= 6, T[j][c] below (A's first six columns are e_j)
+    auto fcol = [&](int c, int j) -> double { return j < 6 ? T[6 * j + c] : F[12 * c + j]; };
     double* Kl = un + KL_OFF;   // K_k (the P update reads it)
     for (int e = lane; e < 144; e += RT) {
       const int i = e / 12, j = e - 12 * i;
@@ -297,10 +298,10 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
       while (loff(i + 1) <= e) ++i;
       j = e - loff(i);
     };
-    int pi0, pj0, pi1, pj1, gc, gd;
+    int pi0, pj0, pi1, pj1, gc, gd;   // (gc, gd): lane's G item, lanes 36..56
     tri(lane, pi0, pj0);
     tri(lane + 64 < 78 ? lane + 64 : 0, pi1, pj1);
-    tri(lane < 21 ? lane : 0, gc, gd);
+    tri(lane >= 36 && lane < 57 ? lane - 36 : 0, gc, gd);
     const bool p1 = lane + 64 < 78;
     // column j of A: extra rows ar1, ar2 with coefficients dt * (x1 + y1 cos
     // + z1 sin), dt * (y2 cos + z2 sin)
@@ -349,34 +350,32 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
       wsync();
       RS_ACC(11, t_fa);
       RS_T(t_fb);
-      // (b) G = 2V + B'T (identity for fixed), F[c][j] = (T'A)[c][j]
+      // (b) in one pass: F[c][j] = (T'A)[c][j] for the columns j >= 6 (lanes
+      // < 36; the columns j < 6 of A are unit vectors, so F[c][j] = T[j][c]
+      // there and is read from T), and the lower triangle of G = 2V + B'T
+      // (lanes 36..56; identity rows/columns for fixed variables)
       {
-        auto gfitem = [&](int e) -> double {
-          if (e < 36) {
-            const int c = e / 6, d = e - 6 * c;
-            double acc = bwk[c] * T[54 + d];
-            acc = fma(bwk[6 + c], T[60 + d], acc);
-            acc = fma(bwk[12 + c], T[66 + d], acc);
-            if (c < 3) {
-              acc = fma(bforce(0, c), T[36 + d], acc);
-              acc = fma(bforce(1, c), T[42 + d], acc);
-              acc = fma(bforce(2, c), T[48 + d], acc);
-            }
-            if (!freec(c)) return c == d ? 1.0 : 0.0;
-            return c == d ? acc + ((k < N - 1) ? 2.0 * kRdiag : 0.0) : acc;
-          }
-          const int e2 = e - 36, c = e2 / 12, j = e2 - 12 * c;
+        if (lane < 36) {
+          const int c = lane / 6, j = 6 + lane - 6 * c;
           const ACol aj = acol(j);
           double f = T[6 * j + c];
           f = fma(aj.x1 + aj.y1 * cp + aj.z1 * sp, T[6 * aj.r1 + c], f);
           f = fma(aj.y2 * cp + aj.z2 * sp, T[6 * aj.r2 + c], f);
-          return f;
-        };
-        const double g0 = gfitem(lane);
-        const double g1 = gfitem(lane < 44 ? lane + 64 : 0);
-        if (lane < 36) G[lane] = g0;
-        else F[lane - 36] = g0;
-        if (lane < 44) F[lane + 28] = g1;
+          F[12 * c + j] = f;
+        } else if (lane < 57) {
+          const int c = gc, d = gd;
+          double acc = bwk[c] * T[54 + d];
+          acc = fma(bwk[6 + c], T[60 + d], acc);
+          acc = fma(bwk[12 + c], T[66 + d], acc);
+          if (c < 3) {
+            acc = fma(bforce(0, c), T[36 + d], acc);
+            acc = fma(bforce(1, c), T[42 + d], acc);
+            acc = fma(bforce(2, c), T[48 + d], acc);
+          }
+          if (!freec(c)) acc = c == d ? 1.0 : 0.0;
+          else if (c == d) acc += (k < N - 1) ? 2.0 * kRdiag : 0.0;
+          G[6 * c + d] = acc;
+        }
       }
       wsync();
       RS_ACC(12, t_fb);
@@ -411,11 +410,18 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
           Di[loff(r) + c] = -s * dinv[r];
         }
       }
-      if (lane < 21) {   // Dinv entry (gc, gd) -- a lane-constant index
-        double v = 0.0;
+      {   // G^-1 = Dinv'Dinv, every entry in every lane; lane e < 21 stores entry e
+        double gv = 0.0;
 #pragma unroll
-        for (int e = 0; e < 21; ++e) v = (e == lane) ? Di[e] : v;
-        Dl[lane] = v;
+        for (int c = 0; c < 6; ++c)
+#pragma unroll
+          for (int d = 0; d <= c; ++d) {
+            double s = 0.0;
+#pragma unroll
+            for (int m = c; m < 6; ++m) s = fma(Di[loff(m) + c], Di[loff(m) + d], s);
+            gv = (loff(c) + d == lane) ? s : gv;
+          }
+        if (lane < 21) gi[21 * k + lane] = gv;
       }
       if (lane < 12) {
         const int j = lane;
@@ -424,7 +430,7 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
         for (int c = 0; c < 6; ++c) {
           double s = 0.0;
 #pragma unroll
-          for (int m = 0; m <= c; ++m) s = fma(Di[loff(c) + m], F[12 * m + j], s);
+          for (int m = 0; m <= c; ++m) s = fma(Di[loff(c) + m], fcol(m, j), s);
           y[c] = s;
         }
 #pragma unroll
@@ -439,15 +445,7 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
       wsync();
       RS_ACC(13, t_fc);
       RS_T(t_fd);
-      // (d) G^-1 (gc, gd) = sum_{m >= gc} Dinv[m][gc] Dinv[m][gd] (lanes < 21);
-      // P_k (i, j), j <= i, mirrored
-      if (lane < 21) {
-        double s = 0.0;
-#pragma unroll
-        for (int m = 0; m < 6; ++m)
-          if (m >= gc) s = fma(Dl[loff(m) + gc], Dl[loff(m) + gd], s);
-        gi[21 * k + lane] = s;
-      }
+      // (d) P_k (i, j), j <= i, mirrored
       if (k == 0) break;
       {
         auto pitem = [&](int i, int j) -> double {
@@ -463,7 +461,7 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
           const double s2 = fma(cb2, r2[aj.r2], fma(cb1, r2[aj.r1], r2[j]));
           double pn = fma(ca2, s2, fma(ca1, s1, s0)) + q;
 #pragma unroll
-          for (int c = 0; c < 6; ++c) pn = fma(-F[12 * c + i], Kl[12 * c + j], pn);
+          for (int c = 0; c < 6; ++c) pn = fma(-fcol(c, i), Kl[12 * c + j], pn);
           return pn;
         };
         const double v0 = pitem(pi0, pj0);
