@@ -465,10 +465,10 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
           return pn;
         };
         const double v0 = pitem(pi0, pj0);
+        const double v1 = pitem(pi1, pj1);   // (lanes >= 14: a duplicate of item 0, not stored)
         Pn[12 * pi0 + pj0] = v0;
         Pn[12 * pj0 + pi0] = v0;
         if (p1) {
-          const double v1 = pitem(pi1, pj1);
           Pn[12 * pi1 + pj1] = v1;
           Pn[12 * pj1 + pi1] = v1;
         }
