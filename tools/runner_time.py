@@ -1,0 +1,33 @@
+"""Wall time of the device Runner (hmpc_runner.Runner.run: plan + gait +
+100 MPC periods of mpcontrol_plan + plant) for the reference's configs[0]
+(run.py 3f --N_run=2000, N = 60) at batch 1 and a few batch sizes.
+python tools/runner_time.py [graph]"""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, 'hopper-mpc-inertial_amd'))
+import hmpc_runner  # noqa: E402
+
+graph = 'graph' in sys.argv[1:]
+res = {}
+for B in (1, 256, 4096):
+    r = hmpc_runner.Runner(dt=1e-3, dyn='3f', curve=False, N_run=2000, N=60, batch=B)
+    kw = dict(record=False)
+    if graph:
+        kw['graph'] = True
+    r.run(n_periods=2, **kw)          # warm (workspaces, code objects)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    out = r.run(**kw)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    r.close()
+    res[B] = {'seconds': el, 'robot_steps_per_s': B * 2000 / el, 'mpc_solves_per_s': B * 101 / el,
+              'all_solved': bool((out['status'] == 0).all())}
+print(json.dumps({'graph': graph, 'runner_N60_2000_steps': res}, indent=1))
