@@ -232,7 +232,7 @@ int check_solve_args(hmpc_ctx* c, int64_t B, const void* x_in, const void* x_lin
 
 extern "C" {
 
-int hmpc_version(void) { return 10000; }
+int hmpc_version(void) { return 10200; }
 
 int hmpc_supported_horizons(int variant, int* Ns, int cap) {
   return hmpc::supported_horizons(variant, Ns, cap);

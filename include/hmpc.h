@@ -89,7 +89,9 @@ extern "C" {
 
 typedef struct hmpc_ctx hmpc_ctx;
 
-/* ABI version (major*10000 + minor*100 + patch) */
+/* ABI version (major*10000 + minor*100 + patch): 1.2.0 = 1.0 + the fp32 dense
+   build, HMPC_PREC_F64_RICCATI / _F64_DENSE / _F32_GENERIC, hmpc_kernel_name,
+   hmpc_active_capacity, hmpc_plan_batch, hmpc_gait_batch, HMPC_VARIANT_CAS */
 int hmpc_version(void);
 
 /* Which horizons have a dedicated (one- or two-wavefront) kernel for
