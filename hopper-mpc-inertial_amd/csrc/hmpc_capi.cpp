@@ -443,6 +443,10 @@ int mpcontrol_impl(hmpc_ctx* c, int64_t B, int init, const double* x_in, const d
                    const double* pf, const double* C, const double* mu, double* x_prev,
                    double* u, double* obj, int32_t* status, int32_t* iters, void* stream,
                    const hmpc::SolveArgs* view) {
+  if (c->variant == HMPC_VARIANT_CAS) {   // its mpcontrol has no init / time shift (cas :112)
+    c->err = "mpcontrol: the CasADi variant solves one QP per call (hmpc_solve_batch)";
+    return HMPC_ERR_UNSUPPORTED;
+  }
   HMPC_HIP(c, hipSetDevice(c->device));
   hipStream_t s = (hipStream_t)stream;
   auto args = [&](int32_t* st, int32_t* it, double* ob, int mode) {
