@@ -650,22 +650,31 @@ solve_kernel(SolveArgs a) {
     //   cost-to-go (wave-uniform) S_N = W_{N-1} = 100 Q, S_t = Q + Ad_t' S_{t+1} Ad_t
     real xr = tid < 12 ? sm[L::XIN + tid] : 0.0;
     const real qr = qdiag(tid);
-    real s[22];
+    // S_t entries 0..11 (translational axes and yaw) lane-parallel: lane
+    // q < 4 holds block q's [pp, pv, vv] (q = 3: yaw [tt, tw, ww]), one
+    // instruction stream for the four blocks.  These blocks do not depend on
+    // the instance; the roll/pitch block (entries 12..21, yaw-dependent) stays
+    // wave-uniform in s[].
+    const real qa = tid == 0 ? kQ[0] : tid == 1 ? kQ[1] : tid == 2 ? kQ[2] : kQ[5];
+    const real qc = tid == 0 ? kQ[6] : tid == 1 ? kQ[7] : tid == 2 ? kQ[8] : kQ[11];
+    real ta = kTermQ * qa, tb = 0.0, tc = kTermQ * qc;
+    real s[10];   // P00 P01 P11 M00 M01 M10 M11 Q00 Q01 Q11 (entries 12..21)
+    s[0] = kTermQ * kQ[3]; s[1] = 0.0; s[2] = kTermQ * kQ[4];
+    s[3] = s[4] = s[5] = s[6] = 0.0;
+    s[7] = kTermQ * kQ[9]; s[8] = 0.0; s[9] = kTermQ * kQ[10];
+    real* const tstore = sm + L::SS + 3 * (tid < 4 ? tid : 0);
+    auto store_s = [&](int t) __attribute__((always_inline)) {
+      if (tid < 4) {
+        tstore[22 * t] = ta;
+        tstore[22 * t + 1] = tb;
+        tstore[22 * t + 2] = tc;
+      }
+      if (tid == 0)
 #pragma unroll
-    for (int a3 = 0; a3 < 3; ++a3) {
-      s[3 * a3] = kTermQ * kQ[a3];
-      s[3 * a3 + 1] = 0.0;
-      s[3 * a3 + 2] = kTermQ * kQ[6 + a3];
-    }
-    s[9] = kTermQ * kQ[5]; s[10] = 0.0; s[11] = kTermQ * kQ[11];
-    s[12] = kTermQ * kQ[3]; s[13] = 0.0; s[14] = kTermQ * kQ[4];
-    s[15] = s[16] = s[17] = s[18] = 0.0;
-    s[19] = kTermQ * kQ[9]; s[20] = 0.0; s[21] = kTermQ * kQ[10];
+        for (int e = 0; e < 10; ++e) sm[L::SS + 22 * t + 12 + e] = s[e];
+    };
     if (tid == 2) sm[L::ZB] = xr;
-    if (tid == 0) {
-#pragma unroll
-      for (int e = 0; e < 22; ++e) sm[L::SS + 22 * (N - 1) + e] = s[e];
-    }
+    store_s(N - 1);
     // stage k's yaw cos/sin from lane k (readlane: no LDS round trip in the
     // recursions' chains).  Both loops are unrolled: the reference rows are
     // loaded up front and the gradient terms d_t stay in registers (lane
@@ -687,41 +696,33 @@ solve_kernel(SolveArgs a) {
       constexpr int t = N - 1 - k;
       if constexpr (t >= 1) {
         const real ct = rdlane(cpl, t), st = rdlane(spl, t);
-        // translational axes and yaw: [[a, b], [b, c]] with p' = p + dt v
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int o = 3 * q;
-          const real aa = s[o], bb = s[o + 1], cc = s[o + 2];
-          s[o + 1] = fma(dt, aa, bb);
-          s[o + 2] = cc + dt * (real(2) * bb + dt * aa);
+        // translational axes and yaw: [[a, b], [b, c]] with p' = p + dt v,
+        // then + W_{t-1} = Q (diagonal)
+        {
+          const real aa = ta, bb = tb, cc = tc;
+          tb = fma(dt, aa, bb);
+          tc = cc + dt * (real(2) * bb + dt * aa);
+          ta = aa + qa;
+          tc = tc + qc;
         }
         // roll/pitch block, theta' = theta + D w with D = dt [[c, s], [-s, c]]:
         //   M' = M + P D,   Qm' = Qm + D'(M + P D) + M' D   (old M in the last term)
         const real D00 = ct * dt, D01 = st * dt, D10 = -st * dt, D11 = ct * dt;
-        const real P00 = s[12], P01 = s[13], P11 = s[14];
-        const real M00 = s[15], M01 = s[16], M10 = s[17], M11 = s[18];
+        const real P00 = s[0], P01 = s[1], P11 = s[2];
+        const real M00 = s[3], M01 = s[4], M10 = s[5], M11 = s[6];
         const real N00 = M00 + (P00 * D00 + P01 * D10), N01 = M01 + (P00 * D01 + P01 * D11);
         const real N10 = M10 + (P01 * D00 + P11 * D10), N11 = M11 + (P01 * D01 + P11 * D11);
         const real A00 = D00 * N00 + D10 * N10, A01 = D00 * N01 + D10 * N11;
         const real A11 = D01 * N01 + D11 * N11;
         const real B00 = M00 * D00 + M10 * D10, B01 = M00 * D01 + M10 * D11;
         const real B11 = M01 * D01 + M11 * D11;
-        s[19] += A00 + B00;
-        s[20] += A01 + B01;
-        s[21] += A11 + B11;
-        s[15] = N00; s[16] = N01; s[17] = N10; s[18] = N11;
-        // + W_{t-1} = Q (diagonal)
-#pragma unroll
-        for (int a3 = 0; a3 < 3; ++a3) {
-          s[3 * a3] += kQ[a3];
-          s[3 * a3 + 2] += kQ[6 + a3];
-        }
-        s[9] += kQ[5]; s[11] += kQ[11];
-        s[12] += kQ[3]; s[14] += kQ[4];
-        s[19] += kQ[9]; s[21] += kQ[10];
-        if (tid == 0)
-#pragma unroll
-          for (int e = 0; e < 22; ++e) sm[L::SS + 22 * (t - 1) + e] = s[e];
+        s[7] += A00 + B00;
+        s[8] += A01 + B01;
+        s[9] += A11 + B11;
+        s[3] = N00; s[4] = N01; s[5] = N10; s[6] = N11;
+        s[0] += kQ[3]; s[2] += kQ[4];
+        s[7] += kQ[9]; s[9] += kQ[10];
+        store_s(t - 1);
       }
     });
     B::sync();

@@ -168,11 +168,39 @@ __device__ __forceinline__ void adt_times(R (&g)[12], R dt, R cp, R sp) {
 
 // The same two maps lane-parallel: lane r < 12 holds component r.  The
 // cross terms come from other lanes (readlane / DPP row shift); lanes >= 12 pass
-// their value through unchanged.
+// their value through unchanged.  Branch-free: d_r = al_r x[r+-6] + sp beta_r
+// with per-lane 0/1 coefficients (no per-lane selects of the terms).  r is
+// the caller's lane (an opaque copy keeps the coefficients from being hoisted
+// out of a persistent loop).
 template <typename R>
-__device__ __forceinline__ R ad_lane(R x, R dt, R cp, R sp) {
+__device__ __forceinline__ R ad_lane(R x, R dt, R cp, R sp, int r = threadIdx.x) {
+  // r < 3: v; r = 3, 4: Rz w (cp w0 + sp w1, cp w1 - sp w0); r = 5: w2
+  const R xv = row_shift<6>(x);   // x[r+6] for r < 6
+  const R w0 = rdlane(x, 9), w1 = rdlane(x, 10);
+  const R k1 = (r == 3 || r == 4) ? R(1) : R(0);
+  const R k0 = (r < 6 && r != 3 && r != 4) ? R(1) : R(0);
+  const R s1 = (r == 3) ? R(1) : R(0), s0 = (r == 4) ? R(-1) : R(0);
+  const R d = fma(fma(k1, cp, k0), xv, sp * fma(s1, w1, s0 * w0));
+  return fma(dt, d, x);
+}
+template <typename R>
+__device__ __forceinline__ R adt_lane(R g, R dt, R cp, R sp, int r = threadIdx.x) {
+  // 6 <= r < 9: g[r-6]; r = 9, 10: Rz' (cp g3 - sp g4, sp g3 + cp g4); r = 11: g5
+  const R gv = row_shift<-6>(g);  // g[r-6] for 6 <= r < 12
+  const R g3 = rdlane(g, 3), g4 = rdlane(g, 4);
+  const R k1 = (r == 9 || r == 10) ? R(1) : R(0);
+  const R k0 = (r >= 6 && r < 12 && r != 9 && r != 10) ? R(1) : R(0);
+  const R s3 = (r == 10) ? R(1) : R(0), s4 = (r == 9) ? R(-1) : R(0);
+  const R d = fma(fma(k1, cp, k0), gv, sp * fma(s3, g3, s4 * g4));
+  return fma(dt, d, g);
+}
+// The select form of the same maps: fewer live lane constants, for the
+// generic kernel whose register budget is already spent (the coefficient form
+// above spills there)
+template <typename R>
+__device__ __forceinline__ R ad_lane_sel(R x, R dt, R cp, R sp) {
   const int r = threadIdx.x;
-  const R xv = row_shift<6>(x);   // x[r+6] for r < 3
+  const R xv = row_shift<6>(x);
   const R w0 = rdlane(x, 9), w1 = rdlane(x, 10), w2 = rdlane(x, 11);
   R d = R(0);
   d = (r < 3) ? xv : d;
@@ -182,9 +210,9 @@ __device__ __forceinline__ R ad_lane(R x, R dt, R cp, R sp) {
   return fma(dt, d, x);
 }
 template <typename R>
-__device__ __forceinline__ R adt_lane(R g, R dt, R cp, R sp) {
+__device__ __forceinline__ R adt_lane_sel(R g, R dt, R cp, R sp) {
   const int r = threadIdx.x;
-  const R gv = row_shift<-6>(g);  // g[r-6] for 6 <= r < 9
+  const R gv = row_shift<-6>(g);
   const R g3 = rdlane(g, 3), g4 = rdlane(g, 4), g5 = rdlane(g, 5);
   R d = R(0);
   d = (r >= 6 && r < 9) ? gv : d;

@@ -229,7 +229,7 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
     const double qr = qdiag(lane);
     if (lane == 2) zb[0] = xr;
     for (int k = 0; k < N; ++k) {
-      xr = ad_lane(xr, dt, cs[2 * k], cs[2 * k + 1]) + ((lane == 8) ? -a.g * dt : 0.0);
+      xr = ad_lane(xr, dt, cs[2 * k], cs[2 * k + 1], lane) + ((lane == 8) ? -a.g * dt : 0.0);
       const double kf = (k == N - 1) ? kTermQ : 1.0;
       if (lane < 12) dd[12 * k + lane] = kf * qr * (xr - un[12 * k + lane]);
       if (lane == 2) zb[k + 1] = xr;
@@ -259,7 +259,7 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
         nb[6 * i + c] = -h;
       }
       if (t >= 2) {
-        ar = adt_lane(ar, dt, cs[2 * i], cs[2 * i + 1]) + (lane < 12 ? dd[12 * (t - 2) + lane] : 0.0);
+        ar = adt_lane(ar, dt, cs[2 * i], cs[2 * i + 1], lane) + (lane < 12 ? dd[12 * (t - 2) + lane] : 0.0);
       }
     }
   }
@@ -1093,7 +1093,7 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
       const double cp = cs[2 * k], sp = cs[2 * k + 1];
       const double* uk = vv + 6 * k;
       const double u0 = uk[0], u1 = uk[1], u2 = uk[2], u3 = uk[3], u4 = uk[4], u5 = uk[5];
-      double nx = ad_lane(xr, dt, cp, sp) + ((lane == 8) ? -a.g * dt : 0.0);
+      double nx = ad_lane(xr, dt, cp, sp, lane) + ((lane == 8) ? -a.g * dt : 0.0);
       if (lane >= 6 && lane < 9) {
         const int r = lane - 6;
         nx += bv<VAR>(r, 0, dtm, cp, sp) * u0 + bv<VAR>(r, 1, dtm, cp, sp) * u1 + bv<VAR>(r, 2, dtm, cp, sp) * u2;

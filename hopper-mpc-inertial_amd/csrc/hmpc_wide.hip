@@ -197,7 +197,7 @@ __device__ void wide_solve(const SolveArgs& a, const int N, const int64_t b, T* 
       for (int e = 0; e < 22; ++e) ss[22 * (N - 1) + e] = s[e];
     for (int k = 0; k < N; ++k) {
       const T cp = cs[2 * k], sp = cs[2 * k + 1];
-      xrr = ad_lane(xrr, dt, cp, sp) + ((tid == 8) ? -T(a.g) * dt : T(0.0));
+      xrr = ad_lane_sel(xrr, dt, cp, sp) + ((tid == 8) ? -T(a.g) * dt : T(0.0));
       const T kf = (k == N - 1) ? T(kTermQ) : T(1.0);
       if (tid < 12) dg[12 * k + tid] = kf * qr * (xrr - xr[12 * k + tid]);
       if (tid == 2) zb[k + 1] = xrr;
@@ -240,7 +240,7 @@ __device__ void wide_solve(const SolveArgs& a, const int N, const int64_t b, T* 
     T ar = tid < 12 ? dg[12 * (N - 1) + tid] : T(0.0);
     if (tid >= 6 && tid < 12) aj[6 * (N - 1) + tid - 6] = ar;
     for (int t = N - 1; t >= 1; --t) {
-      ar = adt_lane(ar, dt, cs[2 * t], cs[2 * t + 1]) + (tid < 12 ? dg[12 * (t - 1) + tid] : T(0.0));
+      ar = adt_lane_sel(ar, dt, cs[2 * t], cs[2 * t + 1]) + (tid < 12 ? dg[12 * (t - 1) + tid] : T(0.0));
       if (tid >= 6 && tid < 12) aj[6 * (t - 1) + tid - 6] = ar;
     }
   }
@@ -727,7 +727,7 @@ __device__ void wide_solve(const SolveArgs& a, const int N, const int64_t b, T* 
         bv_u = (rvv == 0) ? dtm * (cp * u0 - sp * u1) : ((rvv == 1) ? dtm * (sp * u0 + cp * u1) : dtm * u2);
       }
       const T bu = (tid >= 9 && tid < 12) ? bw_u : ((tid >= 6 && tid < 9) ? bv_u : T(0.0));
-      xrr = ad_lane(xrr, dt, cp, sp) + bu + ((tid == 8) ? -T(a.g) * dt : T(0.0));
+      xrr = ad_lane_sel(xrr, dt, cp, sp) + bu + ((tid == 8) ? -T(a.g) * dt : T(0.0));
       const T kf = (k == N - 1) ? T(kTermQ) : T(1.0);
       const T e = xrr - (tid < 12 ? xr[12 * k + tid] : T(0.0));
       objl = fma(kf * qr * e, e, objl);
