@@ -115,6 +115,23 @@ __device__ __forceinline__ int opaque_zero() {
   asm volatile("s_mov_b32 %0, 0" : "=s"(z));
   return z;
 }
+// Per-lane select on a wave-uniform 64-bit lane mask (bit l set: lane l
+// takes t).  With a compile-time mask this is one v_cndmask per 32 bits and
+// an s_mov of the constant -- no v_cmp of the lane id against a step index.
+__device__ __forceinline__ unsigned msel(uint64_t m, unsigned t, unsigned f) {
+  unsigned r;
+  asm("v_cndmask_b32 %0, %1, %2, %3" : "=v"(r) : "v"(f), "v"(t), "s"(m));
+  return r;
+}
+__device__ __forceinline__ double msel(uint64_t m, double t, double f) {
+  const unsigned long long bt = __double_as_longlong(t), bf = __double_as_longlong(f);
+  const unsigned lo = msel(m, (unsigned)bt, (unsigned)bf), hi = msel(m, (unsigned)(bt >> 32), (unsigned)(bf >> 32));
+  return __longlong_as_double(((unsigned long long)hi << 32) | lo);
+}
+__device__ __forceinline__ float msel(uint64_t m, float t, float f) {
+  return __uint_as_float(msel(m, __float_as_uint(t), __float_as_uint(f)));
+}
+typedef __attribute__((address_space(3))) real lds_real;
 
 // LDS loads the scheduler cannot move.  hipcc sinks prefetches next to their
 // use and then waits with lgkmcnt(0); these are issued where they stand, and
@@ -272,7 +289,7 @@ struct Lay {
   static constexpr int TOTAL = ENDA > ENDB ? ENDA : ENDB;
   static_assert(12 * (N + 1) <= LCN, "x* staging does not fit");
   // start of column k of L (rows k..NV-1)
-  __device__ static int cb(int k) { return k * NV - ((k * (k - 1)) >> 1); }
+  __host__ __device__ static constexpr int cb(int k) { return k * NV - ((k * (k - 1)) >> 1); }
 };
 
 __device__ __forceinline__ int loff(int r) { return (r * (r + 1)) >> 1; }
@@ -843,6 +860,7 @@ solve_kernel(SolveArgs a) {
     // non-positive pivots, counted: `if (piv <= 0) status = ...` per step
     // kept 60 condition masks alive in SGPRs (and spilled)
     real nbad = 0.0;
+    uint64_t okall = ~0ull;   // the one-wave path's pivot signs (an SGPR mask)
     auto nld_of = [](int lo, int ch) constexpr {   // b128 loads of chunk ch of [lo, NV)
       return (NV - lo - 8 * ch) >= 8 ? 4 : (NV - lo - 8 * ch + 1) / 2;
     };
@@ -863,6 +881,10 @@ solve_kernel(SolveArgs a) {
       const real dx = diag_extra(tid, my_fixed);   // lane s: the extra of pivot s
       real2 nb[CW / 2];                 // chunk 0 of the next step
       real p_rs = 0.0, p_tk = 0.0;   // next step's 1/L_kk and M[tid][k]
+      // the two column buffers' LDS addresses, held in registers (opaque):
+      // otherwise every step rematerialises them with v_movs
+      unsigned colb[2] = {lds_addr(sm + L::COLB), lds_addr(sm + L::COLB + NT + 8)};
+      asm volatile("" : "+v"(colb[0]), "+v"(colb[1]));
       auto ahead = [&](auto sc) __attribute__((always_inline)) {
         constexpr int s = decltype(sc)::value;
         constexpr int JS = (s + 1) & ~1;
@@ -874,19 +896,22 @@ solve_kernel(SolveArgs a) {
         // don't-care upper-triangle values there, lanes >= NV are never read)
         col[tid] = mine;
         B::sync();
-        const unsigned cb0 = lds_addr(col + JS);
+        const unsigned cb0 = colb[s & 1];
         sfor<0, nldc(JS, 0)>([&](auto ic) __attribute__((always_inline)) {
           constexpr int i = decltype(ic)::value;
-          lds_ld2<2 * RB * i>(nb[i], cb0);
+          lds_ld2<RB * (JS + 2 * i)>(nb[i], cb0);
         });
         const real piv = rdlane(mine + dx, s);
-        const real pv = piv > 0.0 ? piv : 1.0;
-        nbad += (piv > real(0)) ? real(0) : real(1);   // folded into status after the loop
-        pin(nbad);                          // (materialised here, not sunk to the end)
+        const uint64_t pos = __ballot(piv > real(0));   // all lanes or none
+        const real pv = pos ? piv : real(1);
+        okall &= pos;                       // folded into status after the loop
+        asm volatile("" : "+s"(okall));     // (materialised here, not sunk to the end)
         p_rs = rsq_nr(pv);
         p_tk = (mine * p_rs) * p_rs;
       };
       ahead(std::integral_constant<int, 0>{});
+      constexpr uint64_t kLive = NV >= 64 ? ~0ull : ((1ull << NV) - 1);
+      const unsigned tb = lds_addr(sm + tid);
       sfor<0, NV>([&](auto kc) __attribute__((always_inline)) {
         constexpr int k = decltype(kc)::value;
         constexpr int JA = (k + 1) & ~1;   // 16-B aligned start of the update
@@ -894,24 +919,27 @@ solve_kernel(SolveArgs a) {
         constexpr int NAHEAD = (k + 1 < NV) ? 1 + nldc((k + 2) & ~1, 0) : 0;   // LDS ops of ahead()
         constexpr bool kfixed = VAR == 2 && k % 6 == 1;                       // 2f fy
         constexpr bool kforce = k % 6 < 3;
-        const int ko = k + opaque_zero();
         const real rs = p_rs, tk = p_tk;
         lds_wait<0>(nb[0], nb[1]);   // this step's chunk 0 (and everything older)
-        const bool below = tid > ko && tid < NV;
         // every lane updates: a lane <= k changes only its registers > k, the
         // upper triangle of its row (don't-care, overwritten at their step)
         const real nt = -tk;
+        // lane masks of this step, compile-time constants (msel)
+        constexpr uint64_t m_eq = 1ull << k;
+        constexpr uint64_t m_ge = kLive & ~(m_eq - 1);
+        constexpr uint64_t m_gt = m_ge & ~m_eq;
         // branch-free store of column k of M (other lanes: the column buffer
         // of step k+1, which ahead() rewrites after this store)
         {
-          const int o_l = L::LC + L::cb(k) + (tid - ko);
-          const int o_d = L::COLB + ((k + 1) & 1) * (NT + 8) + tid;
-          sm[(tid >= ko && tid < NV) ? o_l : o_d] = (tid == ko) ? rs : tk;
+          constexpr int DOFF = RB * (L::COLB + ((k + 1) & 1) * (NT + 8));
+          constexpr int LOFF = RB * (L::LC + L::cb(k) - k);
+          const unsigned ad = msel(m_ge, tb + (unsigned)(LOFF - DOFF), tb);
+          *(lds_real*)(ad + DOFF) = msel(m_eq, rs, tk);
         }
         // phase 5's forward substitution w = M^-1 (-h) rides along: w_k is
         // final here, rows below take -M[i][k] w_k (off the step's chain)
-        wv = fma(below ? -tk : 0.0, rdlane(wv, k), wv);
-        const unsigned cbase = lds_addr(sm + L::COLB + (k & 1) * (NT + 8) + JA);
+        wv = fma(msel(m_gt, tk, real(0)), -rdlane(wv, k), wv);
+        const unsigned cbase = colb[k & 1];
         // chunks >= 1 go through a 3-deep ring: chunk ch+2 is issued while
         // chunk ch is consumed (one chunk ahead left the LDS latency exposed)
         real2 buf[3][CW / 2];
@@ -920,7 +948,7 @@ solve_kernel(SolveArgs a) {
           if constexpr (ch >= 1 && ch < NCH) {
             sfor<0, nldc(JA, ch)>([&](auto ic) __attribute__((always_inline)) {
               constexpr int i = decltype(ic)::value;
-              lds_ld2<RB * (CW * ch + 2 * i)>(buf[ch % 3][i], cbase);
+              lds_ld2<RB * (JA + CW * ch + 2 * i)>(buf[ch % 3][i], cbase);
             });
           }
         };
@@ -1038,7 +1066,7 @@ solve_kernel(SolveArgs a) {
       });
     }
     __syncthreads();
-    if (nbad != 0.0) status = ST_NUMERICAL;
+    if (nbad != 0.0 || okall == 0) status = ST_NUMERICAL;
     dinv = tid < NV ? sm[L::LC + L::cb(tid < NV ? tid : 0)] : 0.0;   // 1 / L[tid][tid]
   }
   HMPC_STAMP(5);
