@@ -334,9 +334,12 @@ __device__ __forceinline__ real tri_fwd_lds(real acc, const real* Mc, const real
   const int tid = threadIdx.x;
   if constexpr (L::W == 1) {
     // M[tid][s] for tid > s sits at Mc[cb(s) + tid - s]; other lanes read a 0
+    // (the lane mask is built on the scalar unit: no v_cmp per step)
     const unsigned base = lds_addr(Mc + tid), zaddr = lds_addr(zero);
+    constexpr uint64_t kLive = NV >= 64 ? ~0ull : ((1ull << NV) - 1);
     auto addr = [&](int s) -> unsigned {
-      return (tid > s && tid < NV && s < NV) ? base + (unsigned)RB * (unsigned)(L::cb(s) - s) : zaddr;
+      const uint64_t m = s < NV ? kLive & ~((2ull << s) - 1) : 0;   // lanes s+1 .. NV-1
+      return msel(m, base + (unsigned)RB * (unsigned)(L::cb(s) - s), zaddr);
     };
     real ring[4];
     sfor<0, 4>([&](auto jc) __attribute__((always_inline)) {
@@ -411,9 +414,11 @@ __device__ __forceinline__ real tri_bwd(real acc, const real* Mc, const real* ze
   acc *= dinv;
   if constexpr (L::W == 1) {
     // M[s][tid] for tid < s sits at Mc[cbt + s - tid]; other lanes read a 0
+    // (the lane mask is built on the scalar unit: no v_cmp per step)
     const unsigned base = lds_addr(Mc + cbt - tid), zaddr = lds_addr(zero);
     auto addr = [&](int s) -> unsigned {
-      return (tid < s && s < NV && s >= 0) ? base + (unsigned)RB * (unsigned)s : zaddr;
+      const uint64_t m = (s > 0 && s < NV) ? (1ull << s) - 1 : 0;   // lanes 0 .. s-1
+      return msel(m, base + (unsigned)RB * (unsigned)s, zaddr);
     };
     real ring[4];
     sfor<0, 4>([&](auto jc) __attribute__((always_inline)) {
