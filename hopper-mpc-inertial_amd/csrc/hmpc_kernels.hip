@@ -301,6 +301,12 @@ __device__ __forceinline__ int loff(int r) { return (r * (r + 1)) >> 1; }
 #endif
 constexpr int kRing2 = HMPC_RING2;
 static_assert(kRing2 == 4 || kRing2 == 8, "ring depth");
+// and of the one-wave sweeps (one load a step)
+#ifndef HMPC_RING1
+#define HMPC_RING1 4
+#endif
+constexpr int kRing1 = HMPC_RING1;
+static_assert(kRing1 == 4 || kRing1 == 8, "ring depth");
 
 // ----------------------------------------------------------------------------
 // triangular sweeps.  The factor is kept as the unit lower M = L diag(L)^-1,
@@ -341,19 +347,19 @@ __device__ __forceinline__ real tri_fwd_lds(real acc, const real* Mc, const real
       const uint64_t m = s < NV ? kLive & ~((2ull << s) - 1) : 0;   // lanes s+1 .. NV-1
       return msel(m, base + (unsigned)RB * (unsigned)(L::cb(s) - s), zaddr);
     };
-    real ring[4];
-    sfor<0, 4>([&](auto jc) __attribute__((always_inline)) {
+    real ring[kRing1];
+    sfor<0, kRing1>([&](auto jc) __attribute__((always_inline)) {
       lds_ld1(ring[decltype(jc)::value], addr(s0 + decltype(jc)::value));
     });
 #pragma unroll 1
-    for (int s = s0; s < SEND; s += 4) {
-      sfor<0, 4>([&](auto jc) __attribute__((always_inline)) {
+    for (int s = s0; s < NV; s += kRing1) {   // (steps >= NV are no-ops)
+      sfor<0, kRing1>([&](auto jc) __attribute__((always_inline)) {
         constexpr int j = decltype(jc)::value;
         const int sj = s + j;
         const real ys = rdlane(acc, sj);
-        lds_wait<3>(ring[j]);
+        lds_wait<kRing1 - 1>(ring[j]);
         acc = fma(-ring[j], ys, acc);
-        lds_ld1(ring[j], addr(sj + 4));
+        lds_ld1(ring[j], addr(sj + kRing1));
       });
     }
     lds_wait<0>(ring[0]);   // drain the ring (its last loads are dummies)
@@ -408,7 +414,7 @@ __device__ __forceinline__ real tri_bwd(real acc, const real* Mc, const real* ze
                                           real dinv, real* red) {
   using L = Lay<N>;
   constexpr int NV = L::NV;
-  constexpr int STOP = ((NV + 3) & ~3) - 1;   // first step, padded (steps >= NV are no-ops)
+  constexpr int STOP = L::W == 1 ? ((NV + kRing1 - 1) & ~(kRing1 - 1)) - 1 : ((NV + 3) & ~3) - 1;   // first step, padded (steps >= NV are no-ops)
   const int tid = threadIdx.x;
   const int cbt = tid < NV ? L::cb(tid) : 0;
   acc *= dinv;
@@ -420,19 +426,19 @@ __device__ __forceinline__ real tri_bwd(real acc, const real* Mc, const real* ze
       const uint64_t m = (s > 0 && s < NV) ? (1ull << s) - 1 : 0;   // lanes 0 .. s-1
       return msel(m, base + (unsigned)RB * (unsigned)s, zaddr);
     };
-    real ring[4];
-    sfor<0, 4>([&](auto jc) __attribute__((always_inline)) {
+    real ring[kRing1];
+    sfor<0, kRing1>([&](auto jc) __attribute__((always_inline)) {
       lds_ld1(ring[decltype(jc)::value], addr(STOP - decltype(jc)::value));
     });
 #pragma unroll 1
-    for (int s = STOP; s >= 0; s -= 4) {
-      sfor<0, 4>([&](auto jc) __attribute__((always_inline)) {
+    for (int s = STOP; s >= 0; s -= kRing1) {
+      sfor<0, kRing1>([&](auto jc) __attribute__((always_inline)) {
         constexpr int j = decltype(jc)::value;
         const int sj = s - j;
         const real zs = rdlane(acc, sj);
-        lds_wait<3>(ring[j]);
+        lds_wait<kRing1 - 1>(ring[j]);
         acc = fma(-ring[j], zs, acc);
-        lds_ld1(ring[j], addr(sj - 4));
+        lds_ld1(ring[j], addr(sj - kRing1));
       });
     }
     lds_wait<0>(ring[0]);   // drain the ring (its last loads are dummies)
