@@ -795,7 +795,7 @@ solve_kernel(SolveArgs a) {
     for (int r = 0; r < 3; ++r) e0[6 + r] = ci < 3 ? rowm * bv<VAR>(r, ci, dtm, cpi, spi) : 0.0;
 #pragma unroll
     for (int r = 0; r < 3; ++r) e0[9 + r] = rowm * bwi[6 * r + ci];
-    s_times(sm + L::SS + 22 * ii, e0, f);
+    s_times<true>(sm + L::SS + 22 * ii, e0, f);
     // gradient: h_v = 2 b' a_{i+1} (b = Bd_i e_c, a = adjoint of phase 2)
     real hacc = 0.0;
 #pragma unroll
@@ -1409,6 +1409,13 @@ solve_kernel(SolveArgs a) {
     const real qr = qdiag(tid_o);   // (not CSE-d with phase 2's copy)
     const int rw = (tid >= 9 && tid < 12) ? tid - 9 : 0;   // my row of Bd's omega block
     const int rv = (tid >= 6 && tid < 9) ? tid - 6 : 0;    // my row of Bd's velocity block
+    // the objective's terms are branch-free: lanes >= 12 carry qr = 0 (and a
+    // finite x, x_ref), lanes >= 6 a zero input weight, so their products
+    // add exact zeros instead of splitting the wave at every stage
+    const real rdu = tid_o < 6 ? real(kRdiag) : real(0);
+    const int tu = tid_o < 6 ? tid_o : 0;
+    const real ubz = tid_o == 2 ? real(1) : real(0);
+    const real gdt = tid_o == 8 ? -real(a.g) * dt : real(0);
     real objl = 0.0;
     sfor<0, N>([&](auto kc) __attribute__((always_inline)) {
       constexpr int k = decltype(kc)::value;
@@ -1426,15 +1433,15 @@ solve_kernel(SolveArgs a) {
         bv_u = (rv == 0) ? dtm2 * (cp * u0 - sp * u1) : ((rv == 1) ? dtm2 * (sp * u0 + cp * u1) : dtm2 * u2);
       }
       const real bu = (tid >= 9 && tid < 12) ? bw_u : ((tid >= 6 && tid < 9) ? bv_u : 0.0);
-      xr = ad_lane(xr, dt, cp, sp) + bu + ((tid == 8) ? -real(a.g) * dt : real(0));
+      xr = ad_lane(xr, dt, cp, sp) + bu + gdt;
       const real kf = (k == N - 1) ? kTermQ : 1.0;
-      const real e = tid < 12 ? xr - xrg[k] : 0.0;
+      const real e = xr - xrg[k];
       objl = fma(kf * qr * e, e, objl);
-      if (k < N - 1 && tid < 6) {   // (k is a constant here)
+      if constexpr (k < N - 1) {
         const real ub = a.uref_aliased ? ((sm[L::CC + N - 1] != 0.0) ? 2.0 * a.m * a.g : 0.0)
                                          : ((sm[L::CC + k] != 0.0) ? 2.0 * a.m * a.g : 0.0);
-        const real du = uk[tid] - (tid == 2 ? ub : real(0));
-        objl = fma(real(kRdiag) * du, du, objl);
+        const real du = fma(-ubz, ub, uk[tu]);
+        objl = fma(rdu * du, du, objl);
       }
       if (tid < 12) xo[12 * (k + 1) + tid] = xr;
     });

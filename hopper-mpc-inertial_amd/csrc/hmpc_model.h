@@ -126,9 +126,27 @@ __device__ __forceinline__ void wave_argmin(R& v, int& i) {
 //   9..11  yaw: [tt, tw, ww]                 (theta_z = x[5], w_z = x[11])
 //   12..21 roll/pitch block y = (x3, x4, x9, x10):
 //          P00 P01 P11 M00 M01 M10 M11 Q00 Q01 Q11  (M_ij = S[x(3+i)][x(9+j)])
-// f = S e for the structured S (full 12 rows)
-template <typename R>
+// f = S e for the structured S (full 12 rows).  LOWER0: e[0..5] are zero
+// (an input impulse), so their products are skipped rather than multiplied
+// by a zero the compiler may not fold away.
+template <bool LOWER0 = false, typename R>
 __device__ __forceinline__ void s_times(const R* s, const R (&e)[12], R (&f)[12]) {
+  const R P00 = s[12], P01 = s[13], P11 = s[14], M00 = s[15], M01 = s[16], M10 = s[17],
+               M11 = s[18], Q00 = s[19], Q01 = s[20], Q11 = s[21];
+  if constexpr (LOWER0) {
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      f[a] = s[3 * a + 1] * e[6 + a];
+      f[6 + a] = s[3 * a + 2] * e[6 + a];
+    }
+    f[5] = s[10] * e[11];
+    f[11] = s[11] * e[11];
+    f[3] = M00 * e[9] + M01 * e[10];
+    f[4] = M10 * e[9] + M11 * e[10];
+    f[9] = Q00 * e[9] + Q01 * e[10];
+    f[10] = Q01 * e[9] + Q11 * e[10];
+    return;
+  }
 #pragma unroll
   for (int a = 0; a < 3; ++a) {
     f[a] = s[3 * a] * e[a] + s[3 * a + 1] * e[6 + a];
@@ -136,8 +154,6 @@ __device__ __forceinline__ void s_times(const R* s, const R (&e)[12], R (&f)[12]
   }
   f[5] = s[9] * e[5] + s[10] * e[11];
   f[11] = s[10] * e[5] + s[11] * e[11];
-  const R P00 = s[12], P01 = s[13], P11 = s[14], M00 = s[15], M01 = s[16], M10 = s[17],
-               M11 = s[18], Q00 = s[19], Q01 = s[20], Q11 = s[21];
   f[3] = P00 * e[3] + P01 * e[4] + M00 * e[9] + M01 * e[10];
   f[4] = P01 * e[3] + P11 * e[4] + M10 * e[9] + M11 * e[10];
   f[9] = M00 * e[3] + M10 * e[4] + Q00 * e[9] + Q01 * e[10];
@@ -243,7 +259,9 @@ template <int VAR, typename R>
 __device__ __forceinline__ R bd_dot(int c2, const R (&y)[12], const R* bw, R dtm,
                                          R cp, R sp) {
   R acc = R(0);
-  if (c2 < 3) {
+  if constexpr (VAR == 3) {   // dt/m I: one product (no FMAs by structural zeros)
+    if (c2 < 3) acc = dtm * y[6 + c2];
+  } else if (c2 < 3) {
 #pragma unroll
     for (int r = 0; r < 3; ++r) acc = fma(bv<VAR>(r, c2, dtm, cp, sp), y[6 + r], acc);
   }
