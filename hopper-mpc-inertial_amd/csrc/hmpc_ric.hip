@@ -492,6 +492,15 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
   //             x_{k+1}[i] = (A_k x)[i] + B_k[i,:] u_k    (lane i < 12)
   // Every step's data (K_k from the global workspace, B_k / w_k from LDS) is
   // loaded two steps ahead (a three-deep register ring).
+  // acc += x[lane n of the row] * k as ONE instruction: gfx950's 64-bit DPP
+  // (row_newbcast only) broadcasts lane n of each 16-lane row, and every
+  // consumer here is in row 0 (lanes < 12) -- no readlane -> SGPR -> FMA
+  // round trip.  Each block starts with s_nop 4: the compiler does not see
+  // DPP inside asm, so the block covers the worst hazard in front of it
+  // itself -- an SALU write of EXEC (the lane < 6 stores) followed by a DPP
+  // op needs 5 wait states (a VALU write of x, 2).
+#define HMPC_DPPF(acc, x, k, n) "v_fmac_f64_dpp %" #acc ", %" #x ", %" #k " row_newbcast:" #n " row_mask:0xf bank_mask:0xf\n\t"
+#define HMPC_DPPFN(acc, x, k, n) "v_fmac_f64_dpp %" #acc ", %" #x ", -%" #k " row_newbcast:" #n " row_mask:0xf bank_mask:0xf\n\t"
   struct BwdL {
     double cp, sp, st, b0, b1, b2, n, kc[6];
   };
@@ -561,7 +570,6 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
     // ---- backward sweep
     {
       double li = 0.0;                                  // lam_{j+1}[lane]
-      double l6 = 0.0, l7 = 0.0, l8 = 0.0, l9 = 0.0, l10 = 0.0, l11 = 0.0;   // broadcast
       auto bstep = [&](int j, const BwdL& d) __attribute__((always_inline)) {
         double k6, k7, k8;
         if constexpr (VAR == 3) {
@@ -571,26 +579,42 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
           k7 = fma(kQ_[1], d.cp, kS[1] * d.sp);
           k8 = kP[2];
         }
-        const double bc = fma(k6, l6, fma(k7, l7, k8 * l8)) + fma(d.b0, l9, fma(d.b1, l10, d.b2 * l11));
+        // B_j'lam over lam[6..11] (lanes 6..11 of li)
+        double bc;
+        if constexpr (ENT == 1) {
+          double bc0 = 0.0, bc1 = 0.0;
+          asm("s_nop 4\n\t" HMPC_DPPF(0, 2, 3, 6) HMPC_DPPF(1, 2, 4, 7) HMPC_DPPF(0, 2, 5, 8)
+              HMPC_DPPF(1, 2, 6, 9) HMPC_DPPF(0, 2, 7, 10) HMPC_DPPF(1, 2, 8, 11)
+              : "+v"(bc0), "+v"(bc1)
+              : "v"(li), "v"(k6), "v"(k7), "v"(k8), "v"(d.b0), "v"(d.b1), "v"(d.b2));
+          bc = bc0 + bc1;
+        } else {
+          bc = fma(k6, rdlane(li, 6), fma(k7, rdlane(li, 7), k8 * rdlane(li, 8))) +
+               fma(d.b0, rdlane(li, 9), fma(d.b1, rdlane(li, 10), d.b2 * rdlane(li, 11)));
+        }
         const bool fr = lane >= 3 || (d.st != 0.0 && !(VAR == 2 && lane == 1));
         const double m = fr ? d.n - bc : d.n;
         if (lane < 6) mu_[6 * j + lane] = m;
         if (j == 0) return;
-        const double m0 = rdlane(m, 0), m1 = rdlane(m, 1), m2 = rdlane(m, 2);
-        const double m3 = rdlane(m, 3), m4 = rdlane(m, 4), m5 = rdlane(m, 5);
         // (A'lam)[i]: lanes 6..8 += dt lam[i-6]; 9 += dt (c lam3 - s lam4);
         // 10 += dt (s lam3 + c lam4); 11 += dt lam5
         const double s6 = row_shift<-6>(li), s5 = row_shift<-5>(li), s7 = row_shift<-7>(li);
         double a0 = fma(fma(gB, d.cp, gA), s6, li), a1 = (gC * d.sp) * s5, a2 = (gD * d.sp) * s7;
-        a0 = fma(d.kc[0], m0, a0);
-        a1 = fma(d.kc[1], m1, a1);
-        a2 = fma(d.kc[2], m2, a2);
-        a0 = fma(d.kc[3], m3, a0);
-        a1 = fma(d.kc[4], m4, a1);
-        a2 = fma(d.kc[5], m5, a2);
+        // + K_j[:, i]'mu_j, mu_j in lanes 0..5 of m
+        if constexpr (ENT == 1) {
+          asm("s_nop 4\n\t" HMPC_DPPF(0, 3, 4, 0) HMPC_DPPF(1, 3, 5, 1) HMPC_DPPF(2, 3, 6, 2)
+              HMPC_DPPF(0, 3, 7, 3) HMPC_DPPF(1, 3, 8, 4) HMPC_DPPF(2, 3, 9, 5)
+              : "+v"(a0), "+v"(a1), "+v"(a2)
+              : "v"(m), "v"(d.kc[0]), "v"(d.kc[1]), "v"(d.kc[2]), "v"(d.kc[3]), "v"(d.kc[4]), "v"(d.kc[5]));
+        } else {
+          a0 = fma(d.kc[0], rdlane(m, 0), a0);
+          a1 = fma(d.kc[1], rdlane(m, 1), a1);
+          a2 = fma(d.kc[2], rdlane(m, 2), a2);
+          a0 = fma(d.kc[3], rdlane(m, 3), a0);
+          a1 = fma(d.kc[4], rdlane(m, 4), a1);
+          a2 = fma(d.kc[5], rdlane(m, 5), a2);
+        }
         li = lane < 12 ? (a0 + a1) + a2 : 0.0;
-        l6 = rdlane(li, 6); l7 = rdlane(li, 7); l8 = rdlane(li, 8);
-        l9 = rdlane(li, 9); l10 = rdlane(li, 10); l11 = rdlane(li, 11);
       };
       // (loads are unconditional -- out-of-range steps reload stage 0 -- so
       // that the vmcnt/lgkmcnt waits stay counted, not drained)
@@ -645,19 +669,25 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
     {
       double xi = 0.0;   // x_k[lane]
       auto fstep = [&](int k, const FwdL& d) __attribute__((always_inline)) {
-        double xs[12];
-#pragma unroll
-        for (int i = 0; i < 12; ++i) xs[i] = rdlane(xi, i);
+        // u = w - K_k x (x in lanes 0..11 of xi)
         double a0 = d.w, a1 = 0.0;
+        if constexpr (ENT == 1) {
+          asm("s_nop 4\n\t" HMPC_DPPFN(0, 2, 3, 0) HMPC_DPPFN(1, 2, 4, 1) HMPC_DPPFN(0, 2, 5, 2)
+              HMPC_DPPFN(1, 2, 6, 3) HMPC_DPPFN(0, 2, 7, 4) HMPC_DPPFN(1, 2, 8, 5)
+              HMPC_DPPFN(0, 2, 9, 6) HMPC_DPPFN(1, 2, 10, 7) HMPC_DPPFN(0, 2, 11, 8)
+              HMPC_DPPFN(1, 2, 12, 9) HMPC_DPPFN(0, 2, 13, 10) HMPC_DPPFN(1, 2, 14, 11)
+              : "+v"(a0), "+v"(a1)
+              : "v"(xi), "v"(d.kr[0]), "v"(d.kr[1]), "v"(d.kr[2]), "v"(d.kr[3]), "v"(d.kr[4]), "v"(d.kr[5]),
+                "v"(d.kr[6]), "v"(d.kr[7]), "v"(d.kr[8]), "v"(d.kr[9]), "v"(d.kr[10]), "v"(d.kr[11]));
+        } else {
 #pragma unroll
-        for (int c = 0; c < 12; c += 2) {
-          a0 = fma(-d.kr[c], xs[c], a0);
-          a1 = fma(-d.kr[c + 1], xs[c + 1], a1);
+          for (int c = 0; c < 12; c += 2) {
+            a0 = fma(-d.kr[c], rdlane(xi, c), a0);
+            a1 = fma(-d.kr[c + 1], rdlane(xi, c + 1), a1);
+          }
         }
         const double u = a0 + a1;
         if (lane < 6) dst[6 * k + lane] = u;
-        const double u0 = rdlane(u, 0), u1 = rdlane(u, 1), u2 = rdlane(u, 2);
-        const double u3 = rdlane(u, 3), u4 = rdlane(u, 4), u5 = rdlane(u, 5);
         // (A x)[i]: lanes 0..2 += dt x[i+6]; 3 += dt (c x9 + s x10);
         // 4 += dt (c x10 - s x9); 5 += dt x11
         const double s6 = row_shift<6>(xi), s5 = row_shift<5>(xi), s7 = row_shift<7>(xi);
@@ -675,12 +705,20 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
         r2 = fma(m911, d.br[2], r2);
         const double r3 = m911 * d.br[3], r4 = m911 * d.br[4], r5 = m911 * d.br[5];
         double b0 = fma(fma(fB, d.cp, fA), s6, xi), b1 = (fC * d.sp) * s7, b2 = (fD * d.sp) * s5;
-        b0 = fma(r0, u0, b0);
-        b1 = fma(r1, u1, b1);
-        b2 = fma(r2, u2, b2);
-        b0 = fma(r3, u3, b0);
-        b1 = fma(r4, u4, b1);
-        b2 = fma(r5, u5, b2);
+        // + B_k u_k, u_k in lanes 0..5 of u
+        if constexpr (ENT == 1) {
+          asm("s_nop 4\n\t" HMPC_DPPF(0, 3, 4, 0) HMPC_DPPF(1, 3, 5, 1) HMPC_DPPF(2, 3, 6, 2)
+              HMPC_DPPF(0, 3, 7, 3) HMPC_DPPF(1, 3, 8, 4) HMPC_DPPF(2, 3, 9, 5)
+              : "+v"(b0), "+v"(b1), "+v"(b2)
+              : "v"(u), "v"(r0), "v"(r1), "v"(r2), "v"(r3), "v"(r4), "v"(r5));
+        } else {
+          b0 = fma(r0, rdlane(u, 0), b0);
+          b1 = fma(r1, rdlane(u, 1), b1);
+          b2 = fma(r2, rdlane(u, 2), b2);
+          b0 = fma(r3, rdlane(u, 3), b0);
+          b1 = fma(r4, rdlane(u, 4), b1);
+          b2 = fma(r5, rdlane(u, 5), b2);
+        }
         xi = lane < 12 ? (b0 + b1) + b2 : 0.0;
       };
       if constexpr (RING == 3) {
