@@ -506,6 +506,11 @@ __device__ __forceinline__ real tri_bwd(real acc, const real* Mc, const real* ze
 #define HMPC_TOC(slot, v) ((void)0)
 #endif
 
+// issue priority of the chain-bound phases (A/B experiments): 0 off, 1 the
+// Cholesky through the active set, 2 the Cholesky only
+#ifndef HMPC_PRIO
+#define HMPC_PRIO 0
+#endif
 #ifndef HMPC_WAVES_PER_EU
 #define HMPC_WAVES_PER_EU(W) ((W) == 1 ? 2 : 1)
 #endif
@@ -845,6 +850,7 @@ solve_kernel(SolveArgs a) {
   real wv = -hv;   // the forward sweep's accumulator (phase 4)
   __syncthreads();   // union A (XLIN/XREF/PF/S/DG) is dead from here on
   HMPC_STAMP(4);
+  if constexpr (HMPC_PRIO != 0) __builtin_amdgcn_s_setprio(3);
 
   int status = ST_SOLVED;
   real dinv = 0.0;
@@ -1081,6 +1087,7 @@ solve_kernel(SolveArgs a) {
     dinv = tid < NV ? sm[L::LC + L::cb(tid < NV ? tid : 0)] : 0.0;   // 1 / L[tid][tid]
   }
   HMPC_STAMP(5);
+  if constexpr (HMPC_PRIO == 2) __builtin_amdgcn_s_setprio(0);
 
   const real* Lc = sm + L::LC;
   const real* zero = sm + L::ZR;
@@ -1374,6 +1381,7 @@ solve_kernel(SolveArgs a) {
     }
   }
   HMPC_STAMP(7);
+  if constexpr (HMPC_PRIO != 0) __builtin_amdgcn_s_setprio(0);
 
   // an overflowed instance writes nothing but its status and its place in
   // the overflow list (x_lin may be this solve's input, mpcontrol shift)
