@@ -282,11 +282,17 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
     double* Pc = un + PS_OFF;   // P_{k+1}, 12 x 12 full
     double* Pn = un + P2_OFF;   // P_k
     double* T = un + TS_OFF;    // P B, 12 x 6
-    double* F = un + FS_OFF;    // B'P A, 6 x 12
+    double* F = un + FS_OFF;    // (B'P A)' by rows: F[6 j + c] = (B'P A)[c][j], j >= 6
     double* G = un + GS_OFF;    // 6 x 6
-    // F[c][j]: stored for j >= 6, T[j][c] below (A's first six columns are e_j)
-    auto fcol = [&](int c, int j) -> double { return j < 6 ? T[6 * j + c] : F[12 * c + j]; };
-    double* Kl = un + KL_OFF;   // K_k (the P update reads it)
+    // column j of B'P A as a contiguous 6-vector: T's row j for j < 6 (A's
+    // first six columns are e_j), F's row j otherwise; read as 3 b128 loads
+    typedef double dbl2 __attribute__((ext_vector_type(2)));
+    auto col6 = [&](int j, double (&v)[6]) __attribute__((always_inline)) {
+      const dbl2* p = reinterpret_cast<const dbl2*>((j < 6 ? T : F) + 6 * j);
+      const dbl2 v0 = p[0], v1 = p[1], v2 = p[2];
+      v[0] = v0.x; v[1] = v0.y; v[2] = v1.x; v[3] = v1.y; v[4] = v2.x; v[5] = v2.y;
+    };
+    double* Kl = un + KL_OFF;   // K_k by columns (Kl[6 j + c] = K[c][j]; the P update reads it)
     for (int e = lane; e < 144; e += RT) {
       const int i = e / 12, j = e - 12 * i;
       Pc[e] = (i == j) ? 2.0 * kTermQ * kQ[i] : 0.0;
@@ -361,7 +367,7 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
           double f = T[6 * j + c];
           f = fma(aj.x1 + aj.y1 * cp + aj.z1 * sp, T[6 * aj.r1 + c], f);
           f = fma(aj.y2 * cp + aj.z2 * sp, T[6 * aj.r2 + c], f);
-          F[12 * c + j] = f;
+          F[6 * j + c] = f;
         } else if (lane < 57) {
           const int c = gc, d = gd;
           double acc = bwk[c] * T[54 + d];
@@ -425,12 +431,13 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
       }
       if (lane < 12) {
         const int j = lane;
-        double y[6];
+        double y[6], fj[6];
+        col6(j, fj);
 #pragma unroll
         for (int c = 0; c < 6; ++c) {
           double s = 0.0;
 #pragma unroll
-          for (int m = 0; m <= c; ++m) s = fma(Di[loff(c) + m], fcol(m, j), s);
+          for (int m = 0; m <= c; ++m) s = fma(Di[loff(c) + m], fj[m], s);
           y[c] = s;
         }
 #pragma unroll
@@ -439,7 +446,7 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
 #pragma unroll
           for (int m = c; m < 6; ++m) s = fma(Di[loff(m) + c], y[m], s);
           km[72 * k + 12 * c + j] = s;
-          Kl[12 * c + j] = s;
+          Kl[6 * j + c] = s;
         }
       }
       wsync();
@@ -460,8 +467,15 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
           const double s1 = fma(cb2, r1[aj.r2], fma(cb1, r1[aj.r1], r1[j]));
           const double s2 = fma(cb2, r2[aj.r2], fma(cb1, r2[aj.r1], r2[j]));
           double pn = fma(ca2, s2, fma(ca1, s1, s0)) + q;
+          double fi[6], kj[6];
+          col6(i, fi);
+          {
+            const dbl2* kp = reinterpret_cast<const dbl2*>(Kl + 6 * j);
+            const dbl2 k0 = kp[0], k1 = kp[1], k2 = kp[2];
+            kj[0] = k0.x; kj[1] = k0.y; kj[2] = k1.x; kj[3] = k1.y; kj[4] = k2.x; kj[5] = k2.y;
+          }
 #pragma unroll
-          for (int c = 0; c < 6; ++c) pn = fma(-fcol(c, i), Kl[12 * c + j], pn);
+          for (int c = 0; c < 6; ++c) pn = fma(-fi[c], kj[c], pn);
           return pn;
         };
         const double v0 = pitem(pi0, pj0);
