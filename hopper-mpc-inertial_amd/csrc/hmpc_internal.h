@@ -74,6 +74,8 @@ constexpr int ST_OVERFLOW = 4;   // internal: re-solved by the overflow pass
 // SIMD).  Larger active sets go to the overflow pass.
 int ric_qcap(int N);
 int ric_occ(int N);
+// the compile-time horizon the Riccati kernel for N runs with (0: runtime N)
+int ric_static_n(int N);
 // dynamic LDS bytes of the Riccati kernel at horizon N (R in LDS with
 // capacity qcap, or none when qcap == 0: overflow pass)
 size_t ric_lds_bytes(int N, int qcap);

@@ -1259,6 +1259,10 @@ RicCfg ric_config(int N) {
 
 int ric_qcap(int N) { return ric_config(N).cap; }
 int ric_occ(int N) { return ric_config(N).occ; }
+int ric_static_n(int N) {
+  const RicCfg c = ric_config(N);
+  return (N == 60 && c.occ == 1 && c.cap == 47) ? 60 : 0;
+}
 
 // K / G^-1 of every stage, then the cached columns H^-1 n_a (capacity x NV)
 int64_t ric_kws_stride(int N) {
@@ -1288,7 +1292,7 @@ template <int VAR, int OCC>
 bool ric_launch(int N, const SolveArgs& a, hipStream_t s, int* per) {
   const int cap = ric_qcap(N);
   if constexpr (OCC == 1) {
-    if (N == 60 && cap == 47) return ric_launch_k(ric_kernel<VAR, OCC, 60, 47>, N, cap, a, s, per);
+    if (ric_static_n(N) == 60) return ric_launch_k(ric_kernel<VAR, OCC, 60, 47>, N, cap, a, s, per);
   }
   return ric_launch_k(ric_kernel<VAR, OCC>, N, cap, a, s, per);
 }
