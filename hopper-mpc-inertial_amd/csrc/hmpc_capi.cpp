@@ -37,6 +37,9 @@ struct hmpc_ctx {
   // and the global R blocks of its workgroups
   int32_t* ovf = nullptr;
   int64_t ovf_cap = 0;
+  // the counters need a zeroing before the next solve (fresh buffer, or a
+  // solve whose overflow pass -- which zeroes them at its end -- did not run)
+  bool ovf_dirty = true;
   double* rws = nullptr;
   // Riccati kernel: per-workgroup K / G^-1 workspace of its resident grid
   double* kws = nullptr;
@@ -161,6 +164,7 @@ int prepare_ric(hmpc_ctx* c, int64_t B, hmpc::SolveArgs& a) {
     hipError_t e = hipMalloc(&c->ovf, sizeof(int32_t) * (size_t)(B + 4));
     if (e != hipSuccess) { c->err = "overflow list hipMalloc"; return HMPC_ERR_NOMEM; }
     c->ovf_cap = B;
+    c->ovf_dirty = true;
   }
   a.ovf_count = c->ovf;
   a.work = c->ovf + 1;
@@ -189,10 +193,15 @@ int run_solve(hmpc_ctx* c, hmpc::SolveArgs a, hipStream_t s) {
   if (rc != HMPC_OK) return rc;
   rc = prepare_ric(c, a.B, a);
   if (rc != HMPC_OK) return rc;
-  if (a.ovf_count || a.work) {   // overflow count and instance counter
-    hipError_t e = hipMemsetAsync(a.ovf_count ? a.ovf_count : a.work - 1, 0, 2 * sizeof(int32_t), s);
+  // [overflow count | instance counter | overflow-pass done counter]: zeroed
+  // here only when dirty -- the overflow pass, which follows every main pass
+  // that has one, zeroes them at its end (stream order: the next solve's
+  // kernels see them zero).  The CasADi kernel has no overflow pass.
+  if (a.work && (!a.ovf_count || c->ovf_dirty)) {
+    hipError_t e = hipMemsetAsync(a.work - 1, 0, 3 * sizeof(int32_t), s);
     if (e != hipSuccess) return fail_hip(c, e, "hipMemsetAsync(overflow count)");
   }
+  c->ovf_dirty = true;   // until the overflow pass is launched
   if (!hmpc::launch_solve(c->variant, c->N, a, s)) {
     c->err = "no kernel for this (variant, N, precision)";
     return HMPC_ERR_UNSUPPORTED;
@@ -203,6 +212,7 @@ int run_solve(hmpc_ctx* c, hmpc::SolveArgs a, hipStream_t s) {
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail_hip(c, e, "solve launch");
+  c->ovf_dirty = a.ovf_count == nullptr;
   return HMPC_OK;
 }
 

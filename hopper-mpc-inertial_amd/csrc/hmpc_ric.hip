@@ -1225,6 +1225,17 @@ __global__ void __launch_bounds__(RT) ric_overflow_kernel(SolveArgs a, int N) {
     ric_solve<VAR, (6 * kRicNmax + 63) / 64, 3, false>(a2, N, b, ric_sm, Rm, 6 * N, kw, nullptr);
     __syncthreads();
   }
+  // the last workgroup out zeroes [overflow count | instance counter | its
+  // own done counter] for the next solve on this stream (every group read
+  // the count above before it counts itself done): no memset per solve
+  if (threadIdx.x == 0) {
+    __threadfence();
+    if (atomicAdd(a.ovf_count + 2, 1) == (int)gridDim.x - 1) {
+      atomicExch(a.ovf_count, 0);
+      atomicExch(a.ovf_count + 1, 0);
+      atomicExch(a.ovf_count + 2, 0);
+    }
+  }
 }
 
 template <typename K>
