@@ -45,7 +45,9 @@ struct SolveArgs {
   int precision;
   // Active-set overflow (hmpc_ric.hip): an instance whose active set outgrows
   // the LDS capacity of its kernel appends its index to ovf_list (count in
-  // *ovf_count, zeroed before the launch) and is re-solved by the overflow
+  // *ovf_count; ovf_count[1] is the Riccati instance counter, [2] the
+  // overflow pass's done counter: zero at the launch -- the overflow pass
+  // zeroes all three at its end) and is re-solved by the overflow
   // pass with capacity 6N (R in the global workspace rws, rws_stride doubles
   // per resident workgroup).  ovf_count == nullptr: overflow = ST_NUMERICAL.
   int32_t* ovf_count;
