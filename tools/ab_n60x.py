@@ -1,3 +1,7 @@
+"""x* and u* of the N=60 reference-loop replay (tests/golden/loop_3f_N60_config1.npz)
+through libhmpc.so vs libhmpc_prev.so (and any libhmpc_<tag>.so named on the
+command line): a mismatch in x* that u* does not show points at the outputs
+phase or the overflow pass."""
 import os, sys, numpy as np, subprocess
 ROOT='/root/repo'
 code = r'''
@@ -16,7 +20,8 @@ r = cx.solve_host(x_in, x_lin, x_ref, pf, C)
 np.savez(os.environ['OUTF'], u=r['u'], x=r['x'], st=r['status'], it=r.get('iters', r['status']))
 ''' % (ROOT, ROOT, ROOT)
 os.makedirs(ROOT + '/gpurun_out/abx', exist_ok=True)
-for tag, lib in [(t, l) for t, l in (('new', 'libhmpc.so'), ('prev', 'libhmpc_prev.so'), ('nop4', 'libhmpc_nop4.so'),) if os.path.exists(os.path.join(ROOT, 'hopper-mpc-inertial_amd', l))]:
+extra = sys.argv[1:]   # more libhmpc_<tag>.so builds to compare with prev
+for tag, lib in [('new', 'libhmpc.so'), ('prev', 'libhmpc_prev.so')] + [(t, f'libhmpc_{t}.so') for t in extra]:
     env = dict(os.environ, HMPC_LIB=os.path.join(ROOT, 'hopper-mpc-inertial_amd', lib), OUTF=ROOT + f'/gpurun_out/abx/{tag}.npz')
     subprocess.check_call([sys.executable, '-c', code], env=env, timeout=200)
 a = np.load(ROOT + '/gpurun_out/abx/new.npz'); b = np.load(ROOT + '/gpurun_out/abx/prev.npz')
@@ -25,7 +30,7 @@ print('du max', du.max(), 'dx max', dx.max(), 'bad x calls', np.nonzero(dx > 1e-
 i = int(np.argmax(dx)); print('call', i, 'iters new/prev', a['it'][i], b['it'][i], 'status', a['st'][i], b['st'][i])
 d = np.abs(a['x'][i] - b['x'][i]); print('rows with diff', np.nonzero(d.max(1) > 1e-6)[0].tolist()[:10], 'cols', np.nonzero(d.max(0) > 1e-6)[0].tolist())
 print(a['x'][i][-3:], b['x'][i][-3:])
-for tag in ('nop4',):
+for tag in extra:
     f = ROOT + f'/gpurun_out/abx/{tag}.npz'
     if os.path.exists(f):
         c = np.load(f)
