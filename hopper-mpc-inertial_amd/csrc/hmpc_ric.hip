@@ -186,7 +186,7 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
   double* nb = sm + L.NB;
   double* mu_ = sm + L.MU;
   double* km = kw;            // K_k (global workspace)
-  double* gi = kw + 72 * N;   // G_k^-1 (global workspace)
+  double* gi = kw + 72 * N;   // Dinv_k, G_k^-1 = Dinv'Dinv (global workspace, packed lower 21)
   double* ua = sm + L.UA;
   int* act = reinterpret_cast<int*>(sm + L.ACT);
   double* cbv = sm + L.CB;
@@ -421,17 +421,11 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
           Di[loff(r) + c] = -s * dinv[r];
         }
       }
-      {   // G^-1 = Dinv'Dinv, every entry in every lane; lane e < 21 stores entry e
+      {   // Dinv (packed lower) for the sweeps, which apply G^-1 = Dinv'Dinv as
+          // two triangular products: lane e < 21 stores entry e
         double gv = 0.0;
 #pragma unroll
-        for (int c = 0; c < 6; ++c)
-#pragma unroll
-          for (int d = 0; d <= c; ++d) {
-            double s = 0.0;
-#pragma unroll
-            for (int m = c; m < 6; ++m) s = fma(Di[loff(m) + c], Di[loff(m) + d], s);
-            gv = (loff(c) + d == lane) ? s : gv;
-          }
+        for (int e = 0; e < 21; ++e) gv = (e == lane) ? Di[e] : gv;
         if (lane < 21) gi[21 * k + lane] = gv;
       }
       if (lane < 12) {
@@ -665,19 +659,26 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
     }
     for (int i = 6 * (jt + 1) + lane; i < NV; i += RT) mu_[i] = 0.0;
     wsync();
-    // ---- w_j = G_j^-1 mu_j (lane-per-stage; 0 beyond jt)
+    // ---- w_j = G_j^-1 mu_j = Dinv'(Dinv mu_j) (lane-per-stage; 0 beyond jt)
     for (int j = lane; j <= jt; j += RT) {
-      double mv[6], w[6], g[21];
+      double mv[6], y[6], w[6], g[21];
       const double* gj = gi + 21 * j;
 #pragma unroll
       for (int e = 0; e < 21; ++e) g[e] = gj[e];
 #pragma unroll
       for (int c = 0; c < 6; ++c) mv[c] = mu_[6 * j + c];
 #pragma unroll
-      for (int c = 0; c < 6; ++c) {
+      for (int c = 0; c < 6; ++c) {   // y = Dinv mu (lower)
         double s = 0.0;
 #pragma unroll
-        for (int d = 0; d < 6; ++d) s = fma(g[c >= d ? loff(c) + d : loff(d) + c], mv[d], s);
+        for (int d = 0; d <= c; ++d) s = fma(g[loff(c) + d], mv[d], s);
+        y[c] = s;
+      }
+#pragma unroll
+      for (int c = 0; c < 6; ++c) {   // w = Dinv' y
+        double s = 0.0;
+#pragma unroll
+        for (int d = c; d < 6; ++d) s = fma(g[loff(d) + c], y[d], s);
         w[c] = s;
       }
 #pragma unroll
