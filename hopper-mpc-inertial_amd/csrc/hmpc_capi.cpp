@@ -41,7 +41,7 @@ struct hmpc_ctx {
   // solve whose overflow pass -- which zeroes them at its end -- did not run)
   bool ovf_dirty = true;
   double* rws = nullptr;
-  // Riccati kernel: per-workgroup K / G^-1 workspace of its resident grid
+  // Riccati kernel: per-workgroup K / Dinv workspace of its resident grid
   double* kws = nullptr;
   int ric_groups = 0;
   // planner scratch (footstep counter, peak lists)
@@ -118,13 +118,13 @@ int prepare_ws(hmpc_ctx* c, int64_t B, hmpc::SolveArgs& a) {
 }
 
 // Overflow pass geometry: workgroups (each with an R block of capacity 6N and
-// a K / G^-1 workspace in global memory) looping over the instances whose
+// a K / Dinv workspace in global memory) looping over the instances whose
 // active set outgrew the main kernel's capacity.
 constexpr int kOvfGroups = 128;
 
 // Buffers of the dense / Riccati kernels: [overflow count | instance counter |
 // pad | overflow list], the overflow pass's blocks, the Riccati kernel's
-// per-workgroup K / G^-1 workspace.
+// per-workgroup K / Dinv workspace.
 int prepare_ric(hmpc_ctx* c, int64_t B, hmpc::SolveArgs& a) {
   const hmpc::Kernel k = hmpc::pick_kernel(c->variant, c->N, c->precision);
   a.ovf_count = nullptr; a.ovf_list = nullptr; a.rws = nullptr; a.rws_stride = 0;

@@ -55,7 +55,7 @@ struct SolveArgs {
   double* rws;
   int64_t rws_stride;
   // Riccati kernel (persistent): instance counter (zeroed before the launch),
-  // resident workgroups and their K / G^-1 workspace (kws_stride doubles each)
+  // resident workgroups and their K / Dinv workspace (kws_stride doubles each)
   int32_t* work;
   int ric_groups;
   double* kws;
@@ -81,7 +81,7 @@ int ric_static_n(int N);
 // dynamic LDS bytes of the Riccati kernel at horizon N (R in LDS with
 // capacity qcap, or none when qcap == 0: overflow pass)
 size_t ric_lds_bytes(int N, int qcap);
-int64_t ric_kws_stride(int N);   // per-workgroup K / G^-1 workspace (doubles)
+int64_t ric_kws_stride(int N);   // per-workgroup K / Dinv workspace (doubles)
 int64_t ric_rws_stride(int N);   // per-workgroup overflow block: R (6N capacity) + workspace
 int ric_groups(int variant, int N);   // resident workgroups of the main Riccati kernel
 bool launch_solve_ric(int variant, int N, const SolveArgs& a, hipStream_t stream);

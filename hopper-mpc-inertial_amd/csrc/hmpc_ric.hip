@@ -79,9 +79,9 @@ struct RicLay {
 constexpr int PS_OFF = 0, P2_OFF = 144, TS_OFF = 288, FS_OFF = 360, GS_OFF = 432, DL_OFF = 468,
               KL_OFF = 490;
 
-// Global workspace of one workgroup (doubles): K_k [6][12] and G_k^-1 (packed
-// lower) of every stage -- written by the factorisation, read by every sweep
-// (L2-resident: a few workgroups per CU)
+// Global workspace of one workgroup (doubles): K_k [6][12] and Dinv_k (packed
+// lower; G_k^-1 = Dinv_k' Dinv_k) of every stage -- written by the
+// factorisation, read by every sweep
 __host__ __device__ inline int64_t ric_kws_doubles(int N) { return ((93 * (int64_t)N) + 15) & ~(int64_t)15; }
 
 __device__ __forceinline__ int loff(int r) { return (r * (r + 1)) >> 1; }
@@ -99,7 +99,7 @@ __device__ __forceinline__ int wave_imax63(int x) {
 
 // Ordering point between lanes of the one wavefront of a workgroup: LDS
 // instructions of a wave execute in order, so only the compiler must be kept
-// from reordering them.  Global-memory hand-offs between lanes (the K / G^-1
+// from reordering them.  Global-memory hand-offs between lanes (the K / Dinv
 // workspace, the overflow pass's R) use gsync() = a workgroup barrier.
 __device__ __forceinline__ void wsync() { __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront"); }
 __device__ __forceinline__ void gsync() { __syncthreads(); }
@@ -492,7 +492,7 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
     }
     if (nbad != 0.0) status = ST_NUMERICAL;
   }
-  gsync();   // K, G^-1 (global) visible to every lane of the workgroup
+  gsync();   // K, Dinv (global) visible to every lane of the workgroup
 
   // ---------------- H^-1 by two sweeps ----------------------------------------
   // dst = H^-1 NB (NB kept; MU scratch).  Lanes 0..11 hold the 12 state
@@ -1189,7 +1189,7 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
   }
 }
 
-// Persistent: a.ric_groups workgroups, each with its slot of the K / G^-1
+// Persistent: a.ric_groups workgroups, each with its slot of the K / Dinv
 // workspace, take instances off an atomic counter (a.work, zeroed with the
 // overflow count before the launch) until the batch is done.
 // OCC = waves per SIMD the register allocation is held to (2: <= 256 VGPRs +
@@ -1212,7 +1212,7 @@ __global__ void __launch_bounds__(RT) __attribute__((amdgpu_waves_per_eu(OCC, OC
 }
 
 // the overflow pass: instances listed in a.ovf_list, capacity 6N, R and the
-// K / G^-1 workspace in the global block of the workgroup (rws_stride doubles)
+// K / Dinv workspace in the global block of the workgroup (rws_stride doubles)
 template <int VAR>
 __global__ void __launch_bounds__(RT) ric_overflow_kernel(SolveArgs a, int N) {
   extern __shared__ __attribute__((aligned(16))) double ric_sm[];
@@ -1276,7 +1276,7 @@ int ric_static_n(int N) {
   return (N == 60 && c.occ == 1 && c.cap == 47) ? 60 : 0;
 }
 
-// K / G^-1 of every stage, then the cached columns H^-1 n_a (capacity x NV)
+// K / Dinv of every stage, then the cached columns H^-1 n_a (capacity x NV)
 int64_t ric_kws_stride(int N) {
   return ric_kws_doubles(N) + ((((int64_t)ric_qcap(N) * 6 * N) + 15) & ~(int64_t)15);
 }
