@@ -120,3 +120,46 @@ def test_overflow_mpcontrol_shift_in_place(hm):
     cx.close()
     assert np.array_equal(r['status'], o2['status'].cpu().numpy())
     np.testing.assert_array_equal(r['u'], o2['u'].cpu().numpy())
+
+
+@pytest.mark.parametrize('N', [10, 20])
+def test_counters_reset_between_solves(hm, N):
+    """The overflow pass zeroes [overflow count | Riccati instance counter] at
+    its end instead of a memset before every solve (hmpc_ric.hip,
+    ric_overflow_kernel).  Back-to-back solves on ONE context -- an
+    overflowing batch, a normal one, the overflowing one again, on the device
+    entry point and the host one -- must equal fresh-context solves bit for
+    bit; a stale counter would skip instances or re-solve stale list ids."""
+    import hmpc_plan
+    c = hmpc_plan.runner_constants()
+    adv = adversarial(48, N, 2, 50.0, 8.0, mu=0.2)   # overflows (test_overflow_n10)
+    nor = hmpc_plan.sample_instances(300, N, curve=True, seed=9)
+    keys = ('x_in', 'x_lin', 'x_ref', 'pf', 'C', 'mu')
+
+    def ctx():
+        return hm.Context('3f', N, t=c['t'], m=c['m'], g=c['g'], mu=1.0, Jinv=c['Jinv'], rh=c['rh'])
+
+    def dev_solve(cx, inst):
+        d = {k: torch.from_numpy(np.ascontiguousarray(inst[k])).cuda() for k in keys}
+        o = cx.solve_device(d['x_in'], d['x_lin'], d['x_ref'], d['pf'], d['C'], mu=d['mu'])
+        torch.cuda.synchronize()
+        return {k: o[k].cpu().numpy() for k in ('u', 'obj', 'status')}
+
+    def host_solve(cx, inst):
+        r = cx.solve_host(*(inst[k] for k in keys[:5]), mu=inst['mu'])
+        return {k: r[k] for k in ('u', 'obj', 'status')}
+
+    fresh = {}
+    for name, inst in (('adv', adv), ('nor', nor)):
+        cx = ctx()
+        fresh[name] = dev_solve(cx, inst)
+        cx.close()
+    assert (fresh['nor']['status'] == 0).all()
+    cx = ctx()
+    seq = [('adv', dev_solve), ('nor', dev_solve), ('adv', host_solve), ('nor', host_solve),
+           ('adv', dev_solve), ('adv', dev_solve), ('nor', dev_solve)]
+    for name, fn in seq:
+        r = fn(cx, adv if name == 'adv' else nor)
+        for k in ('u', 'obj', 'status'):
+            assert np.array_equal(r[k], fresh[name][k]), (name, fn.__name__, k)
+    cx.close()
