@@ -91,8 +91,8 @@ def workload_label(args, world):
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
-    ap.add_argument('--steps', type=int, default=20)
-    ap.add_argument('--warmup', type=int, default=3)
+    ap.add_argument('--steps', type=int, default=100)
+    ap.add_argument('--warmup', type=int, default=20)
     ap.add_argument('--batch', type=int, default=65536, help='instances per GPU (weak scaling)')
     ap.add_argument('--global-batch', type=int, default=0,
                     help='fixed global batch split over the ranks (strong scaling)')
