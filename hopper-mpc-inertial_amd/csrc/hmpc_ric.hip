@@ -421,12 +421,13 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
           Di[loff(r) + c] = -s * dinv[r];
         }
       }
-      {   // Dinv (packed lower) for the sweeps, which apply G^-1 = Dinv'Dinv as
-          // two triangular products: lane e < 21 stores entry e
-        double gv = 0.0;
+      // Dinv (packed lower) for the sweeps, which apply G^-1 = Dinv'Dinv as
+      // two triangular products: every lane holds all 21 entries, lane 0
+      // stores them (no per-lane select chain)
+      if (lane == 0) {
+        double* g = gi + 21 * k;
 #pragma unroll
-        for (int e = 0; e < 21; ++e) gv = (e == lane) ? Di[e] : gv;
-        if (lane < 21) gi[21 * k + lane] = gv;
+        for (int e = 0; e < 21; ++e) g[e] = Di[e];
       }
       if (lane < 12) {
         const int j = lane;
