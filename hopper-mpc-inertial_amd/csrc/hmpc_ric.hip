@@ -320,12 +320,18 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
       int r1, r2;
       double x1, y1, z1, y2, z2;
     };
+    // branch-free: j is a per-lane value, and an if/else chain here compiled
+    // to divergent branches that reloaded spilled SGPRs on every path
     auto acol = [&](int j) -> ACol {
-      ACol c{j, j, 0.0, 0.0, 0.0, 0.0, 0.0};
-      if (j >= 6 && j < 9) { c.r1 = j - 6; c.x1 = dt; }
-      else if (j == 9) { c.r1 = 3; c.r2 = 4; c.y1 = dt; c.z2 = -dt; }
-      else if (j == 10) { c.r1 = 3; c.r2 = 4; c.z1 = dt; c.y2 = dt; }
-      else if (j == 11) { c.r1 = 5; c.x1 = dt; }
+      const bool v = j >= 6 && j < 9, w9 = j == 9, w10 = j == 10, w11 = j == 11, w = w9 || w10;
+      ACol c;
+      c.r1 = v ? j - 6 : (w ? 3 : (w11 ? 5 : j));
+      c.r2 = w ? 4 : j;
+      c.x1 = (v || w11) ? dt : 0.0;
+      c.y1 = w9 ? dt : 0.0;
+      c.z1 = w10 ? dt : 0.0;
+      c.y2 = w10 ? dt : 0.0;
+      c.z2 = w9 ? -dt : 0.0;
       return c;
     };
     wsync();
