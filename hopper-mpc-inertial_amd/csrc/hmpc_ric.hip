@@ -246,22 +246,20 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
       const int i = t - 1;
       const double a6 = rdlane(ar, 6), a7 = rdlane(ar, 7), a8 = rdlane(ar, 8);
       const double a9 = rdlane(ar, 9), a10 = rdlane(ar, 10), a11 = rdlane(ar, 11);
-      if (lane < 6) {
-        const int c = lane;
+      {   // lanes c < 6 (branch-free; the others compute a copy of input 0)
+        const int c = lane < 6 ? lane : 0;
         const double cp = cs[2 * i], sp = cs[2 * i + 1];
         const double* bwi = bw + 18 * i;
         double acc = bwi[c] * a9 + bwi[6 + c] * a10 + bwi[12 + c] * a11;
-        if (c < 3)
-          acc += bv<VAR>(0, c, dtm, cp, sp) * a6 + bv<VAR>(1, c, dtm, cp, sp) * a7 +
-                 bv<VAR>(2, c, dtm, cp, sp) * a8;
+        const double af = bv<VAR>(0, c, dtm, cp, sp) * a6 + bv<VAR>(1, c, dtm, cp, sp) * a7 +
+                          bv<VAR>(2, c, dtm, cp, sp) * a8;
+        acc = c < 3 ? acc + af : acc;
         const bool stance = cc[i] != 0.0;
         const bool fr = c >= 3 || (stance && !(VAR == 2 && c == 1));
-        double h = fr ? 2.0 * acc : 0.0;
-        if (fr && c == 2 && i < N - 1) {
-          const double ub = a.uref_aliased ? ubar_alias : (stance ? 2.0 * a.m * a.g : 0.0);
-          h -= 2.0 * kRdiag * ub;
-        }
-        nb[6 * i + c] = -h;
+        const double ub = a.uref_aliased ? ubar_alias : (stance ? 2.0 * a.m * a.g : 0.0);
+        const double hz = 2.0 * acc - 2.0 * kRdiag * ub;
+        const double h = fr ? ((c == 2 && i < N - 1) ? hz : 2.0 * acc) : 0.0;
+        if (lane < 6) nb[6 * i + c] = -h;
       }
       if (t >= 2) {
         ar = adt_lane(ar, dt, cs[2 * i], cs[2 * i + 1], lane) + (lane < 12 ? dd[12 * (t - 2) + lane] : 0.0);
