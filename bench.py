@@ -229,7 +229,9 @@ def main():
     # N > 1: the exchange step (per-instance cost + status) is one
     # all-gather of a packed [obj | status] slot on a side stream, pipelined
     # with the next step's solve (double-buffered slots, hmpc_dist)
-    ex = hmpc_dist.ResultExchange(B, dev) if world > 1 else None
+    counts = [hmpc_dist.strong_shard(args.global_batch, world, r)[1] for r in range(world)] \
+        if args.global_batch else None
+    ex = hmpc_dist.ResultExchange(B, dev, counts=counts) if world > 1 else None
     last = [out]
 
     def step(ev=None):
@@ -285,7 +287,7 @@ def main():
             assert ex.calls['all_gather_into_tensor'] == args.warmup + args.steps, ex.calls
             assert ex.calls['all_gather_list'] == 0, ex.calls
         dist_info = {'world_size': dist.get_world_size(), 'backend': backend,
-                     'exchange_calls': ex.calls, 'exchange_bytes_per_rank_per_step': 12 * B}
+                     'exchange_calls': ex.calls, 'exchange_bytes_per_rank_per_step': ex.slot}
 
     base = parity = None
     if rank == 0 and world == 1:

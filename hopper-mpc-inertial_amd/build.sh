@@ -42,7 +42,7 @@ $HIPCC $FLAGS -c csrc/hmpc_cas.hip -o $BDIR/hmpc_cas.o "$@" &
 pids+=($!)
 $HIPCC $FLAGS -c csrc/hmpc_wide.hip -o $BDIR/hmpc_wide.o "$@" &
 pids+=($!)
-$HIPCC $FLAGS -c csrc/hmpc_ric.hip -o $BDIR/hmpc_ric.o "$@" &
+$HIPCC $FLAGS -c ${RIC_SRC:-csrc/hmpc_ric.hip} -o $BDIR/hmpc_ric.o "$@" &
 pids+=($!)
 for p in "${pids[@]}"; do wait "$p"; done
 objs=""

@@ -48,6 +48,12 @@ struct hmpc_ctx {
   void* plan_scratch = nullptr;
   int64_t plan_scratch_bytes = 0;
   hipStream_t own_stream = nullptr;
+  // cross-stream ordering: the workspaces and self-resetting counters above
+  // are per context, so a solve issued on another stream than the last one
+  // first waits for the last one's completion event (no silent race)
+  hipEvent_t last_ev = nullptr;
+  hipStream_t last_stream = nullptr;
+  bool has_last = false;
 };
 
 namespace {
@@ -216,6 +222,29 @@ int run_solve(hmpc_ctx* c, hmpc::SolveArgs a, hipStream_t s) {
   return HMPC_OK;
 }
 
+// Before work on stream s: when the context's last solve went to another
+// stream, s waits for it (the context's workspaces and counters are shared by
+// every stream).  After: the solve's completion event, on s.
+int order_stream(hmpc_ctx* c, hipStream_t s) {
+  if (c->has_last && c->last_stream != s) {
+    hipError_t e = hipStreamWaitEvent(s, c->last_ev, 0);
+    if (e != hipSuccess) return fail_hip(c, e, "hipStreamWaitEvent(last solve of this context)");
+  }
+  return HMPC_OK;
+}
+
+int mark_stream(hmpc_ctx* c, hipStream_t s) {
+  if (!c->last_ev) {
+    hipError_t e = hipEventCreateWithFlags(&c->last_ev, hipEventDisableTiming);
+    if (e != hipSuccess) return fail_hip(c, e, "hipEventCreate");
+  }
+  hipError_t e = hipEventRecord(c->last_ev, s);
+  if (e != hipSuccess) return fail_hip(c, e, "hipEventRecord(solve done)");
+  c->last_stream = s;
+  c->has_last = true;
+  return HMPC_OK;
+}
+
 __global__ void combine_status(int64_t B, const int32_t* s1, const int32_t* i1, int32_t* s2,
                                int32_t* i2) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -280,6 +309,7 @@ int hmpc_destroy(hmpc_ctx* c) {
   if (c->kws) (void)hipFree(c->kws);
   if (c->plan_scratch) (void)hipFree(c->plan_scratch);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+  if (c->last_ev) (void)hipEventDestroy(c->last_ev);
   delete c;
   return HMPC_OK;
 }
@@ -290,10 +320,9 @@ int hmpc_active_capacity(hmpc_ctx* c) {
   if (!c) return -1;
   switch (hmpc::pick_kernel(c->variant, c->N, c->precision)) {
     case hmpc::Kernel::Dense:
-    case hmpc::Kernel::DenseF32: {
-      const int nv = 6 * c->N, q = c->N <= 10 ? 20 : 48;
-      return nv < 20 ? nv : q;   // QMAX of hmpc_kernels.hip
-    }
+      return hmpc::dense_qmax(c->N, false);
+    case hmpc::Kernel::DenseF32:
+      return hmpc::dense_qmax(c->N, true);
     case hmpc::Kernel::Riccati:
       return hmpc::ric_qcap(c->N);
     case hmpc::Kernel::Cas:
@@ -309,15 +338,10 @@ const char* hmpc_kernel_name(hmpc_ctx* c) {
   if (!c) return "";
   const bool v3 = c->variant == HMPC_VARIANT_3F;
   switch (hmpc::pick_kernel(c->variant, c->N, c->precision)) {
-    case hmpc::Kernel::Dense: {
-      static const char* names[2][3] = {
-          {"hmpc::solve_kernel<2, 5, double>", "hmpc::solve_kernel<2, 10, double>", "hmpc::solve_kernel<2, 20, double>"},
-          {"hmpc::solve_kernel<3, 5, double>", "hmpc::solve_kernel<3, 10, double>", "hmpc::solve_kernel<3, 20, double>"}};
-      const int i = c->N == 5 ? 0 : (c->N == 10 ? 1 : 2);
-      return names[v3][i];
-    }
+    case hmpc::Kernel::Dense:
+      return hmpc::dense_name(c->variant, c->N, false);
     case hmpc::Kernel::DenseF32:
-      return v3 ? "hmpc::solve_kernel<3, 10, float>" : "hmpc::solve_kernel<2, 10, float>";
+      return hmpc::dense_name(c->variant, c->N, true);
     case hmpc::Kernel::Cas:
       return "hmpc::cas_kernel";
     case hmpc::Kernel::Riccati:
@@ -359,7 +383,9 @@ int hmpc_solve_batch(hmpc_ctx* c, int64_t B, const double* x_in, const double* x
   if (rc != HMPC_OK || B == 0) return rc;
   HMPC_HIP(c, hipSetDevice(c->device));
   hmpc::SolveArgs a = make_args(c, B, x_in, x_lin, x_ref, pf, C, mu, u, x, obj, status, iters, 0);
-  return run_solve(c, a, (hipStream_t)stream);
+  if ((rc = order_stream(c, (hipStream_t)stream)) != HMPC_OK) return rc;
+  if ((rc = run_solve(c, a, (hipStream_t)stream)) != HMPC_OK) return rc;
+  return mark_stream(c, (hipStream_t)stream);
 }
 
 int hmpc_time_solve_batch(hmpc_ctx* c, int64_t B, const double* x_in, const double* x_lin,
@@ -372,6 +398,7 @@ int hmpc_time_solve_batch(hmpc_ctx* c, int64_t B, const double* x_in, const doub
   HMPC_HIP(c, hipSetDevice(c->device));
   hipStream_t s = (hipStream_t)stream;
   hmpc::SolveArgs a = make_args(c, B, x_in, x_lin, x_ref, pf, C, mu, u, x, obj, status, iters, 0);
+  if ((rc = order_stream(c, s)) != HMPC_OK) return rc;
   rc = run_solve(c, a, s);   // validates the combination and sizes the workspaces
   if (rc != HMPC_OK) return rc;
   struct Ev {   // destroyed on every exit path
@@ -386,6 +413,7 @@ int hmpc_time_solve_batch(hmpc_ctx* c, int64_t B, const double* x_in, const doub
     if (rc != HMPC_OK) return rc;
   }
   HMPC_HIP(c, hipEventRecord(e1.e, s));
+  if ((rc = mark_stream(c, s)) != HMPC_OK) return rc;
   HMPC_HIP(c, hipEventSynchronize(e1.e));
   float t = 0.f;
   HMPC_HIP(c, hipEventElapsedTime(&t, e0.e, e1.e));
@@ -445,6 +473,7 @@ int hmpc_solve_batch_host(hmpc_ctx* c, int64_t B, const double* x_in, const doub
   HMPC_HIP(c, hipMemcpyAsync(status, d_st, 4 * B, hipMemcpyDeviceToHost, s));
   if (iters) HMPC_HIP(c, hipMemcpyAsync(iters, d_it, 4 * B, hipMemcpyDeviceToHost, s));
   HMPC_HIP(c, hipStreamSynchronize(s));
+  c->has_last = false;   // drained: nothing of this context is in flight
   return HMPC_OK;
 }
 
@@ -462,6 +491,8 @@ int mpcontrol_impl(hmpc_ctx* c, int64_t B, int init, const double* x_in, const d
   }
   HMPC_HIP(c, hipSetDevice(c->device));
   hipStream_t s = (hipStream_t)stream;
+  int rc = order_stream(c, s);
+  if (rc != HMPC_OK) return rc;
   auto args = [&](int32_t* st, int32_t* it, double* ob, int mode) {
     hmpc::SolveArgs a = make_args(c, B, x_in, x_prev, x_ref, pf, C, mu, u, x_prev, ob, st, it, mode);
     if (view) {
@@ -471,7 +502,6 @@ int mpcontrol_impl(hmpc_ctx* c, int64_t B, int init, const double* x_in, const d
     }
     return a;
   };
-  int rc;
   if (init) {
     if (B > c->scratch_n) {
       if (c->scratch_i32) (void)hipFree(c->scratch_i32);
@@ -495,7 +525,7 @@ int mpcontrol_impl(hmpc_ctx* c, int64_t B, int init, const double* x_in, const d
     if ((rc = run_solve(c, args(status, iters, obj, 2), s)) != HMPC_OK) return rc;
   }
   HMPC_HIP(c, hipGetLastError());
-  return HMPC_OK;
+  return mark_stream(c, s);
 }
 
 }  // namespace
@@ -592,9 +622,27 @@ int hmpc_plan_batch(hmpc_ctx* c, int64_t B, int N_run, int N_k, double dt, int c
     if (e != hipSuccess) { c->err = "planner scratch hipMalloc"; return HMPC_ERR_NOMEM; }
     c->plan_scratch_bytes = need;
   }
-  hmpc::launch_plan(B, N_run, N_k, dt, curve, t_p, phi_switch, t_start, step_adjustment, x_in, xf, x_ref,
-                    pf_ref, C_map, c->plan_scratch, (hipStream_t)stream);
+  int rc = order_stream(c, (hipStream_t)stream);   // the planner scratch is per context
+  if (rc != HMPC_OK) return rc;
+  if (!hmpc::launch_plan(B, N_run, N_k, dt, curve, t_p, phi_switch, t_start, step_adjustment, x_in, xf,
+                         x_ref, pf_ref, C_map, c->plan_scratch, (hipStream_t)stream)) {
+    c->err = "planner launch";
+    return HMPC_ERR_HIP;
+  }
   HMPC_HIP(c, hipGetLastError());
+  if ((rc = mark_stream(c, (hipStream_t)stream)) != HMPC_OK) return rc;
+  // once per run, not per solve: wait for the plan and read its error word
+  // (the reference raises IndexError in these cases: src/robotrunner.py:211-223)
+  int32_t err = 0;
+  HMPC_HIP(c, hipMemcpyAsync(&err, hmpc::plan_error_word(B, N_run + N_k, c->plan_scratch), sizeof(err),
+                             hipMemcpyDeviceToHost, (hipStream_t)stream));
+  HMPC_HIP(c, hipStreamSynchronize((hipStream_t)stream));
+  if (err) {
+    c->err = std::string("plan: ") + ((err & 1) ? "more footstep peaks than the device planner keeps (64); " : "") +
+             ((err & 2) ? "peak + step_adjustment outside the plan (reference: IndexError); " : "") +
+             ((err & 4) ? "footstep counter past the end of idx_pf (reference: IndexError)" : "");
+    return HMPC_ERR_ARG;
+  }
   return HMPC_OK;
 }
 

@@ -16,10 +16,16 @@
 
 namespace hmpc {
 
-#define HMPC_DECL(n) bool launch_solve_n##n(int variant, const SolveArgs& a, hipStream_t s);
+#define HMPC_DECL(n)                                                       \
+  bool launch_solve_n##n(int variant, const SolveArgs& a, hipStream_t s); \
+  int qmax_solve_n##n();                                                  \
+  const char* name_solve_n##n(int variant);
 HMPC_HORIZON_LIST(HMPC_DECL)
 #undef HMPC_DECL
-#define HMPC_DECL(n) bool launch_solve_n##n##_f32(int variant, const SolveArgs& a, hipStream_t s);
+#define HMPC_DECL(n)                                                           \
+  bool launch_solve_n##n##_f32(int variant, const SolveArgs& a, hipStream_t s); \
+  int qmax_solve_n##n##_f32();                                                  \
+  const char* name_solve_n##n##_f32(int variant);
 HMPC_F32_LIST(HMPC_DECL)
 #undef HMPC_DECL
 
@@ -90,6 +96,36 @@ bool launch_solve(int variant, int N, const SolveArgs& a, hipStream_t s) {
     default:
       return false;
   }
+}
+
+int dense_qmax(int N, bool f32) {
+  if (f32) {
+#define HMPC_CASE(n) \
+  if (N == n) return qmax_solve_n##n##_f32();
+    HMPC_F32_LIST(HMPC_CASE)
+#undef HMPC_CASE
+    return -1;
+  }
+#define HMPC_CASE(n) \
+  if (N == n) return qmax_solve_n##n();
+  HMPC_HORIZON_LIST(HMPC_CASE)
+#undef HMPC_CASE
+  return -1;
+}
+
+const char* dense_name(int variant, int N, bool f32) {
+  if (f32) {
+#define HMPC_CASE(n) \
+  if (N == n) return name_solve_n##n##_f32(variant);
+    HMPC_F32_LIST(HMPC_CASE)
+#undef HMPC_CASE
+    return "";
+  }
+#define HMPC_CASE(n) \
+  if (N == n) return name_solve_n##n(variant);
+  HMPC_HORIZON_LIST(HMPC_CASE)
+#undef HMPC_CASE
+  return "";
 }
 
 bool horizon_supported(int variant, int N) {

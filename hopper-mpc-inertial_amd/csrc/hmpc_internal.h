@@ -162,6 +162,9 @@ int64_t plan_scratch_bytes(int64_t B, int T);
 bool launch_plan(int64_t B, int N_run, int N_k, double dt, int curve, double t_p, double phi_switch,
                  double t_start, int step_adjustment, const double* x_in, const double* xf, double* x_ref,
                  double* pf_ref, double* C_map, void* scratch, hipStream_t s);
+// the planner's device error word inside its scratch (nonzero: the reference
+// would raise IndexError or keep more footstep peaks than fit)
+const int32_t* plan_error_word(int64_t B, int T, const void* scratch);
 bool launch_gait(int n_steps, int mpc_factor, int N, double dt, double mpc_dt, double t_p,
                  double phi_switch, double t_start, double t0, double* C_calls, double* s_hist,
                  hipStream_t s);
@@ -175,6 +178,10 @@ Kernel pick_kernel(int variant, int N, int precision);
 bool launch_solve(int variant, int N, const SolveArgs& a, hipStream_t stream);
 // the generic-horizon kernel (any 1 <= N <= kWideNmax); a.ws must be set
 bool launch_solve_wide(int variant, int N, const SolveArgs& a, hipStream_t stream);
+// the dedicated dense kernel's active-set capacity (-1: none) and name, as
+// its own object reports them (hmpc_kernels.hip)
+int dense_qmax(int N, bool f32);
+const char* dense_name(int variant, int N, bool f32);
 bool horizon_supported(int variant, int N);   // compiled, or generic (N <= kWideNmax)
 bool horizon_compiled(int variant, int N);    // a dedicated one-wavefront kernel
 int supported_horizons(int variant, int* Ns, int cap);

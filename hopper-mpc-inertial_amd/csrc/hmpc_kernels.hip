@@ -1505,5 +1505,16 @@ bool HMPC_CAT(HMPC_CAT(launch_solve_n, HMPC_INST_N), HMPC_LAUNCH_SUFFIX)(int var
   }
   return false;
 }
+// this object's active-set capacity and kernel names (hmpc_active_capacity,
+// hmpc_kernel_name: read from here, not restated in the C API)
+#define HMPC_STR2(x) #x
+#define HMPC_STR(x) HMPC_STR2(x)
+int HMPC_CAT(HMPC_CAT(qmax_solve_n, HMPC_INST_N), HMPC_LAUNCH_SUFFIX)() { return Lay<HMPC_INST_N>::QMAX; }
+const char* HMPC_CAT(HMPC_CAT(name_solve_n, HMPC_INST_N), HMPC_LAUNCH_SUFFIX)(int variant) {
+  // (the template arguments as rocprofv3 demangles them)
+  if (variant == 3) return "hmpc::solve_kernel<3, " HMPC_STR(HMPC_INST_N) ", " HMPC_STR(HMPC_REAL) ">";
+  if (variant == 2) return "hmpc::solve_kernel<2, " HMPC_STR(HMPC_INST_N) ", " HMPC_STR(HMPC_REAL) ">";
+  return "";
+}
 
 }  // namespace hmpc

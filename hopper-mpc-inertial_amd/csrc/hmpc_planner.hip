@@ -31,12 +31,25 @@ namespace {
 
 constexpr int kMaxPeaks = 64;   // footstep indices per robot (a 2000-step run has 5)
 
-// Runner.gait_scheduler (src/robotrunner.py:166-172): np.mod of a positive
-// float64 is fmod; swing when the phase exceeds phi_switch
+// Runner.gait_scheduler (src/robotrunner.py:166-172): np.mod(x, 1), swing
+// when the phase exceeds phi_switch.  np.mod follows the divisor's sign:
+// fmod, then + 1 for a negative remainder (numpy's npy_divmod), so t < t0
+// gives the reference's phase in [0, 1)
+__device__ __forceinline__ double np_mod1(double x) {
+  double r = fmod(x, 1.0);
+  if (r != 0.0 && r < 0.0) r += 1.0;
+  return r;
+}
 __device__ __forceinline__ double gait_state(double t, double t0, double t_p, double phi_switch) {
-  const double ph = fmod((t - t0) / t_p, 1.0);
+  const double ph = np_mod1((t - t0) / t_p);
   return ph > phi_switch ? 0.0 : 1.0;
 }
+
+// device error word of hmpc_plan_batch (HMPC_ERR_ARG on the host): cases in
+// which the reference raises IndexError or keeps more than this kernel can
+constexpr int kErrPeaks = 1;      // more footstep peaks than kMaxPeaks
+constexpr int kErrPeakIdx = 2;    // peak + step_adjustment outside [-T, T)
+constexpr int kErrFootIdx = 4;    // footstep counter past the end of idx_pf
 
 // np.linspace(start, stop, num) row i, component c (numpy 2.x: when any
 // component's step is zero the whole array takes the y = (i / div) * delta
@@ -72,6 +85,7 @@ struct PlanArgs {
   double* C_map;        // [T] (optional)
   int32_t* kf;          // [T] scratch: footstep counter after step k
   int32_t* peaks;       // [B][kMaxPeaks + 2] scratch: idx_pf, count at [kMaxPeaks + 1]
+  int32_t* err;         // [1] error bits (kErr*), zeroed before the launch
 };
 
 // height profile (:207): x_in[2] + amp + amp sin(2 pi / period (i dt) + phi)
@@ -121,7 +135,12 @@ __global__ void plan_peaks_kernel(PlanArgs a) {
       if (xa < xi) {
         int p = (i + (ia - 1)) / 2 + a.step_adjustment;
         if (p < 0) p += n;   // a negative numpy index counts from the end
+        if (p < 0 || p >= n) {   // numpy: IndexError when x_ref[idx_pf[kf]] is read
+          atomicOr(a.err, kErrPeakIdx);
+          p = p < 0 ? 0 : n - 1;
+        }
         if (m < kMaxPeaks) pk[m++] = p;
+        else atomicOr(a.err, kErrPeaks);   // the reference keeps every peak
         i = ia;
         xm1 = -height(a, x0, i - 1);
         xi = xa;
@@ -181,7 +200,10 @@ __global__ void plan_rows_kernel(PlanArgs a) {
     pf[1] = 0.0;
   } else {
     int kf = a.kf[i];
-    if (kf > n_idx - 1) kf = n_idx - 1;   // the reference would index past idx_pf here
+    if (kf > n_idx - 1) {   // the reference raises IndexError past the end of idx_pf
+      atomicOr(a.err, kErrFootIdx);
+      kf = n_idx - 1;
+    }
     const int j = pk[kf];
     pf[0] = row_val(a, x0, x1, anyzero, j, 0);
     pf[1] = row_val(a, x0, x1, anyzero, j, 1);
@@ -216,7 +238,7 @@ __global__ void gait_calls_kernel(GaitArgs a) {
 }  // namespace
 
 int64_t plan_scratch_bytes(int64_t B, int T) {
-  return (int64_t)sizeof(int32_t) * (T + B * (kMaxPeaks + 2));
+  return (int64_t)sizeof(int32_t) * (T + B * (kMaxPeaks + 2) + 1);   // + the error word
 }
 
 bool launch_plan(int64_t B, int N_run, int N_k, double dt, int curve, double t_p, double phi_switch,
@@ -241,11 +263,17 @@ bool launch_plan(int64_t B, int N_run, int N_k, double dt, int curve, double t_p
   a.C_map = C_map;
   a.kf = static_cast<int32_t*>(scratch);
   a.peaks = a.kf + a.T;
+  a.err = a.peaks + B * (kMaxPeaks + 2);
+  if (hipMemsetAsync(a.err, 0, sizeof(int32_t), s) != hipSuccess) return false;
   hipLaunchKernelGGL(plan_scan_kernel, dim3(1), dim3(64), 0, s, a);
   hipLaunchKernelGGL(plan_peaks_kernel, dim3((unsigned)((B + 63) / 64)), dim3(64), 0, s, a);
   const int64_t n = B * a.T;
   hipLaunchKernelGGL(plan_rows_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a);
   return true;
+}
+
+const int32_t* plan_error_word(int64_t B, int T, const void* scratch) {
+  return static_cast<const int32_t*>(scratch) + T + B * (kMaxPeaks + 2);
 }
 
 bool launch_gait(int n_steps, int mpc_factor, int N, double dt, double mpc_dt, double t_p,

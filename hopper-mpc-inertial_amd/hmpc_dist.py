@@ -48,7 +48,8 @@ def allgather_results(obj: torch.Tensor, status: torch.Tensor, out_obj=None, out
 class ResultExchange:
     """The exchange step of a repeated batched solve, pipelined.
 
-    Each slot is ONE byte buffer per rank, ``[obj (8n B) | status (4n B)]``:
+    Each slot is ONE byte buffer per rank, ``[obj (8n B) | status (4n B)]``
+    (n = the largest rank's count, padded to 8 B):
     the solve writes its objective and status straight into the slot's views
     (``outputs()``), and ``exchange()`` all-gathers the whole buffer -- one
     collective per step instead of two.  On CUDA/RCCL the all-gather runs on
@@ -59,14 +60,28 @@ class ResultExchange:
     in rank order.  On gloo (the CPU tests) the exchange is synchronous.
     """
 
-    def __init__(self, n: int, device, nslots: int = 2):
+    def __init__(self, n: int, device, nslots: int = 2, counts=None):
+        """n: this rank's instance count.  counts: every rank's count (rank
+        order) when they differ -- a strong-scaling shard of a global batch
+        the world size does not divide (hmpc_dist.strong_shard).  Every
+        rank's slot is then sized to the largest count, since the collective
+        needs equal sizes; results() trims the padding."""
         self.n, self.world = n, dist.get_world_size()
+        self.counts = list(counts) if counts is not None else [n] * self.world
+        if len(self.counts) != self.world or self.counts[dist.get_rank()] != n:
+            raise ValueError(f'counts {self.counts} do not match rank {dist.get_rank()} with n = {n}')
+        self.cap = max(self.counts)
+        # bytes per rank: [obj 8 cap | status 4 cap], padded to 8 B so every
+        # rank's row of the gathered buffer is float64-aligned
+        self.slot = 8 * self.cap + ((4 * self.cap + 7) // 8) * 8
         self.device = torch.device(device)
         self.cuda = self.device.type == 'cuda'
         self.nslots = nslots
-        self.send = [torch.empty(12 * n, dtype=torch.uint8, device=self.device)
+        # unused tail of a short rank's slot: zero, so the padding that
+        # travels is deterministic
+        self.send = [torch.zeros(self.slot, dtype=torch.uint8, device=self.device)
                      for _ in range(nslots)]
-        self.recv = [torch.empty(self.world * 12 * n, dtype=torch.uint8, device=self.device)
+        self.recv = [torch.empty(self.world * self.slot, dtype=torch.uint8, device=self.device)
                      for _ in range(nslots)]
         self.stream = torch.cuda.Stream(self.device) if self.cuda else None
         self.done = [None] * nslots
@@ -84,7 +99,8 @@ class ResultExchange:
         if self.cuda and self.done[s] is not None:
             torch.cuda.current_stream(self.device).wait_event(self.done[s])
         buf = self.send[s]
-        return buf[:8 * self.n].view(torch.float64), buf[8 * self.n:].view(torch.int32)
+        c8 = 8 * self.cap
+        return buf[:8 * self.n].view(torch.float64), buf[c8:c8 + 4 * self.n].view(torch.int32)
 
     def exchange(self) -> int:
         """All-gather the slot the last ``outputs()`` handed out; returns it."""
@@ -109,7 +125,7 @@ class ResultExchange:
             self.calls['all_gather_into_tensor'] += 1
         else:
             self.calls['all_gather_list'] += 1
-            dist.all_gather(list(self.recv[s].view(self.world, 12 * self.n).unbind(0)),
+            dist.all_gather(list(self.recv[s].view(self.world, self.slot).unbind(0)),
                             self.send[s])
 
     def wait(self):
@@ -121,8 +137,10 @@ class ResultExchange:
                     cur.wait_event(d)
 
     def results(self, slot: int):
-        """(obj [world*n] float64, status [world*n] int32) of a slot, rank order."""
-        r = self.recv[slot].view(self.world, 12 * self.n)
-        obj = r[:, :8 * self.n].contiguous().view(torch.float64).reshape(-1)
-        st = r[:, 8 * self.n:].contiguous().view(torch.int32).reshape(-1)
+        """(obj [sum counts] float64, status [sum counts] int32) of a slot, in
+        rank order (each rank's padding trimmed)."""
+        r = self.recv[slot].view(self.world, self.slot)
+        c8 = 8 * self.cap
+        obj = torch.cat([r[i, :8 * c].contiguous().view(torch.float64) for i, c in enumerate(self.counts)])
+        st = torch.cat([r[i, c8:c8 + 4 * c].contiguous().view(torch.int32) for i, c in enumerate(self.counts)])
         return obj, st

@@ -101,8 +101,11 @@ int hmpc_version(void);
    by a backward Riccati recursion), 64 < N <= 128 by the generic dense kernel.
    Every solve with N <= 64 re-solves the rare instances whose active set
    outgrows its kernel's capacity in an overflow pass (capacity 6N).  The
-   context's workspaces are shared by its calls: calls on one context are
-   expected to be stream-ordered. */
+   context's workspaces and counters are shared by its calls, so the context
+   orders them itself: a call on a different stream than the context's last
+   one first makes its stream wait for that call's completion event
+   (hipStreamWaitEvent).  Calls on one context never overlap; use one context
+   per stream for concurrent solves. */
 int hmpc_supported_horizons(int variant, int* Ns, int cap);
 
 /* Mpc.__init__: t = MPC sampling time (s), N = horizon, m (kg), g (m/s^2),
@@ -191,7 +194,11 @@ int hmpc_convert_batch(hmpc_ctx* ctx, int64_t B, const double* X, double* x, voi
    the --curve plan with the reference's quirks (:193-201).  t_p, phi_switch,
    t_start and step_adjustment are the Runner's gait constants (:44-49,78-79);
    C_map [T] (optional) receives gait_map(T, dt, t_start, 0) (:213).  Feeds
-   hmpc_mpcontrol_plan_batch with plan_bstride = T.  Asynchronous. */
+   hmpc_mpcontrol_plan_batch with plan_bstride = T.  Synchronous on `stream`
+   (once per run): returns HMPC_ERR_ARG where the reference raises IndexError
+   (a footstep peak moved outside the plan by step_adjustment, or a footstep
+   counter past the end of idx_pf, :211-223) or a robot has more than 64
+   footstep peaks; the plan is then not valid. */
 int hmpc_plan_batch(hmpc_ctx* ctx, int64_t B, int N_run, int N_k, double dt, int curve, double t_p,
                     double phi_switch, double t_start, int step_adjustment, const double* x_in,
                     const double* xf, double* x_ref, double* pf_ref, double* C_map, void* stream);
@@ -212,7 +219,7 @@ int hmpc_gait_batch(hmpc_ctx* ctx, int n_steps, int mpc_factor, int N, double dt
 int hmpc_set_precision(hmpc_ctx* ctx, int precision);
 
 /* Name of the solve kernel this context's (variant, N, precision) runs on,
-   e.g. "hmpc::solve_kernel<3, 10>" or "hmpc::ric_kernel<3, 2>" (static string;
+   e.g. "hmpc::solve_kernel<3, 10, double>" or "hmpc::ric_kernel<3, 2, 0, 0>" (static string;
    "" when none).  For benchmark records and profiles. */
 const char* hmpc_kernel_name(hmpc_ctx* ctx);
 

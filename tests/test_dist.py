@@ -59,8 +59,17 @@ def _worker(rank, world, port, q):
     # strong scaling: a fixed global batch in contiguous shards
     gstart, gcount = hmpc_dist.strong_shard(2 * PER_RANK + 1, world, rank)
     sobj, sst = _solve(gstart, gcount)
+    # ... exchanged with uneven per-rank counts (world does not divide the
+    # global batch): slots sized to the largest shard, padding trimmed
+    counts = [hmpc_dist.strong_shard(2 * PER_RANK + 1, world, r)[1] for r in range(world)]
+    assert len(set(counts)) == 2
+    ux = hmpc_dist.ResultExchange(gcount, 'cpu', counts=counts)
+    o, s = ux.outputs()
+    o.copy_(torch.from_numpy(sobj))
+    s.copy_(torch.from_numpy(sst))
+    uobj, ust = ux.results(ux.exchange())
     q.put((rank, oa.numpy().copy(), sa.numpy().copy(), po.numpy().copy() / 3, ps.numpy().copy() - 2,
-           gstart, gcount, sobj, sst))
+           gstart, gcount, sobj, sst, uobj.numpy().copy(), ust.numpy().copy()))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -93,3 +102,72 @@ def test_sharded_allgather_equals_single_process(world):
     assert shards[1][0] + shards[1][1] == 2 * PER_RANK + 1
     assert np.array_equal(np.concatenate([sh[2] for sh in shards]), gobj)
     assert np.array_equal(np.concatenate([sh[3] for sh in shards]), gst)
+    for r in res:   # the uneven exchange: every rank holds the whole global batch
+        assert np.array_equal(r[9], gobj)
+        assert np.array_equal(r[10], gst)
+
+
+class _FakeNccl:
+    """Stands in for torch.distributed on the nccl (RCCL) backend, rank 0 of
+    a world of 3 with uneven counts: all_gather_into_tensor fills every
+    rank's slot, the other ranks' with a payload built from their rank."""
+
+    def __init__(self, counts, rank=0):
+        self.counts, self.rank, self.seen = counts, rank, []
+
+    def get_world_size(self):
+        return len(self.counts)
+
+    def get_rank(self):
+        return self.rank
+
+    def get_backend(self):
+        return 'nccl'
+
+    @staticmethod
+    def payload(r, n, cap):
+        buf = torch.zeros(8 * cap + ((4 * cap + 7) // 8) * 8, dtype=torch.uint8)
+        buf[:8 * n].view(torch.float64).copy_(torch.arange(n, dtype=torch.float64) + 1000.0 * r)
+        buf[8 * cap:8 * cap + 4 * n].view(torch.int32).copy_(torch.full((n,), r, dtype=torch.int32))
+        return buf
+
+    def all_gather_into_tensor(self, out, inp):
+        cap = max(self.counts)
+        slot = 8 * cap + ((4 * cap + 7) // 8) * 8
+        self.seen.append((out.numel(), inp.numel(), out.dtype, inp.dtype, out.is_contiguous()))
+        assert out.numel() == len(self.counts) * inp.numel() == len(self.counts) * slot
+        v = out.view(len(self.counts), slot)
+        for r, n in enumerate(self.counts):
+            v[r].copy_(inp if r == self.rank else self.payload(r, n, cap))
+
+    def all_gather(self, *a, **k):
+        raise AssertionError('the nccl path must not take the list all-gather')
+
+
+def test_nccl_exchange_buffer_views(monkeypatch):
+    """The RCCL branch of ResultExchange._gather (never executed on this
+    CPU-only box) builds the right buffers: one all_gather_into_tensor per
+    step of world x 12 cap bytes, obj / status views at the right offsets,
+    results() trimming each rank's padding."""
+    import hmpc_dist
+    counts = [5, 4, 4]
+    fake = _FakeNccl(counts)
+    monkeypatch.setattr(hmpc_dist, 'dist', fake)
+    ex = hmpc_dist.ResultExchange(counts[0], 'cpu', counts=counts)
+    assert ex.backend == 'nccl' and ex.cap == 5
+    for step in range(3):
+        o, s = ex.outputs()
+        assert o.numel() == 5 and s.numel() == 5 and o.dtype == torch.float64 and s.dtype == torch.int32
+        o.copy_(torch.arange(5, dtype=torch.float64) + 0.5 * step)
+        s.copy_(torch.full((5,), 7, dtype=torch.int32))
+        slot = ex.exchange()
+    assert ex.calls == {'all_gather_into_tensor': 3, 'all_gather_list': 0}
+    assert all(sz == (3 * 64, 64, torch.uint8, torch.uint8, True) for sz in fake.seen)
+    obj, st = ex.results(slot)
+    assert obj.numel() == st.numel() == sum(counts)
+    np.testing.assert_array_equal(obj[:5].numpy(), np.arange(5) + 1.0)
+    np.testing.assert_array_equal(obj[5:9].numpy(), np.arange(4) + 1000.0)
+    np.testing.assert_array_equal(obj[9:].numpy(), np.arange(4) + 2000.0)
+    np.testing.assert_array_equal(st.numpy(), [7] * 5 + [1] * 4 + [2] * 4)
+    with pytest.raises(ValueError):
+        hmpc_dist.ResultExchange(4, 'cpu', counts=counts)   # rank 0 holds 5

@@ -82,3 +82,41 @@ def test_active_capacity(hm):
     assert make(hm, 60).active_capacity == 47
     assert make(hm, 10, 'f64_riccati').active_capacity == 50
     assert make(hm, 10, 'f64_generic').active_capacity == 0
+
+
+@pytest.mark.parametrize('N', [10, 20])
+def test_one_context_two_streams_is_ordered(hm, N):
+    """The context's workspaces and self-resetting counters are shared by its
+    calls; a solve issued on another stream waits for the context's last one
+    (hmpc_capi.cpp order_stream).  Alternating two batches over two streams of
+    one context -- overflowing instances included, so the counters are live --
+    gives exactly what fresh contexts give."""
+    import hmpc_plan as hp
+    from test_gpu_overflow import adversarial
+    B = 2048
+    a = hp.sample_instances(B, N, curve=True, seed=11, mu_sweep=(0.3, 1.2))
+    b = adversarial(B, N, 4, 30.0, 5.0)
+    dv = lambda inst: {k: torch.from_numpy(np.ascontiguousarray(inst[k])).cuda()
+                       for k in ('x_in', 'x_lin', 'x_ref', 'pf', 'C', 'mu')}
+    da, db = dv(a), dv(b)
+    ref = []
+    for d in (da, db):
+        cx = make(hm, N)
+        o = cx.solve_device(d['x_in'], d['x_lin'], d['x_ref'], d['pf'], d['C'], mu=d['mu'])
+        torch.cuda.synchronize()
+        ref.append({k: v.cpu().numpy() for k, v in o.items()})
+        cx.close()
+    cx = make(hm, N)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    outs = []
+    for rep in range(4):
+        for d, s in ((da, s1), (db, s2)):
+            outs.append(cx.solve_device(d['x_in'], d['x_lin'], d['x_ref'], d['pf'], d['C'], mu=d['mu'],
+                                        stream=s.cuda_stream))
+    torch.cuda.synchronize()
+    cx.close()
+    assert (ref[0]['status'] == 0).mean() > 0.9 and (ref[1]['status'] == 0).mean() > 0.5
+    for i, o in enumerate(outs):
+        r = ref[i % 2]
+        for k in ('u', 'x', 'obj', 'status'):
+            assert np.array_equal(o[k].cpu().numpy(), r[k]), (i, k)

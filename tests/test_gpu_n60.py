@@ -99,3 +99,5 @@ def test_n60_batch_statuses_equal_port(hm):
     assert (ref['status'] == 0).sum() == B - 25
     ok = ref['status'] == 0
     assert np.abs(gpu['u'][ok] - ref['u'][ok]).max() <= U_TOL
+    assert np.abs(gpu['x'][ok] - ref['x'][ok]).max() <= U_TOL
+    assert (np.abs(gpu['obj'][ok] - ref['obj'][ok]) / np.abs(ref['obj'][ok])).max() <= 1e-8

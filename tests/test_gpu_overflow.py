@@ -55,6 +55,14 @@ def active_rows(N, inst, ref, i):
     return int(act.sum())
 
 
+def check_x_obj(gpu, ref):
+    """x* (the next call's linearisation, src/mpc_cvx_euler_3f.py:58,68) and
+    the objective of an overflowed instance come from the overflow pass."""
+    assert np.abs(gpu['x'] - ref['x']).max() <= U_TOL
+    rel = np.abs(gpu['obj'] - ref['obj']) / np.maximum(np.abs(ref['obj']), 1.0)
+    assert rel.max() <= 1e-8, rel.max()
+
+
 def solve_both(hm, N, inst, precision):
     import hmpc_plan
     from oracle import port
@@ -80,6 +88,7 @@ def test_overflow_n10(hm, precision, kernel):
     assert (ref['status'] == 0).all()
     assert np.array_equal(gpu['status'], ref['status'])
     assert np.abs(gpu['u'] - ref['u']).max() <= U_TOL
+    check_x_obj(gpu, ref)
     nact = [active_rows(N, inst, ref, i) for i in range(B)]
     assert max(nact) > cap, nact
 
@@ -92,6 +101,7 @@ def test_overflow_n60(hm):
     assert (ref['status'] == 0).all()
     assert np.array_equal(gpu['status'], ref['status'])
     assert np.abs(gpu['u'] - ref['u']).max() <= U_TOL
+    check_x_obj(gpu, ref)
     nact = [active_rows(N, inst, ref, i) for i in range(8)]
     assert max(nact) > cap, (cap, nact)
 

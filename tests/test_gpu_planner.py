@@ -109,3 +109,43 @@ def test_gait_schedule(cx):
     # the reference-recorded rows (gait_map(10, mpc_dt, ts, 0) at the loop's times)
     n = len(g['gait_ts'])
     np.testing.assert_array_equal(C[:n], g['gait_C10'])
+
+
+def test_gait_schedule_before_t0(cx):
+    """t < t0: np.mod((t - t0) / t_p, 1) is in [0, 1) (numpy follows the
+    divisor's sign), so the device gait must not take fmod's negative phase."""
+    import hmpc_plan as hp
+    cfg = hp.RunnerConfig(N_run=400, N=10)
+    n_steps, mf, t0 = 400, cfg.mpc_factor, 0.37
+    C, s_hist = cx.gait_device(n_steps, mf, 10, cfg.dt, cfg.mpc_dt, cfg.t_p, cfg.phi_switch, cfg.t_start,
+                               t0=t0)
+    torch.cuda.synchronize()
+    t = cfg.t_start
+    rows, s = [], []
+    for k in range(n_steps):
+        t = t + cfg.dt
+        s.append(hp.gait_scheduler(cfg, t, t0))
+        if k % mf == 0:
+            rows.append(hp.gait_map(cfg, 10, cfg.mpc_dt, t, t0))
+    np.testing.assert_array_equal(C.cpu().numpy(), np.array(rows))
+    np.testing.assert_array_equal(s_hist.cpu().numpy(), np.array(s, dtype=np.float64))
+    assert (np.array(s) == 0.0).any() and (np.array(s) == 1.0).any()
+
+
+def test_plan_index_errors_are_reported(cx):
+    """Where the reference raises IndexError (a footstep peak pushed outside
+    the plan by step_adjustment, src/robotrunner.py:211-216) hmpc_plan_batch
+    returns HMPC_ERR_ARG instead of a silently clamped plan."""
+    import hmpc
+    import hmpc_plan as hp
+    cfg = hp.RunnerConfig(N_run=2000, N=10)
+    x0, xf = hp.initial_states(cfg)
+    d = lambda a: torch.from_numpy(np.ascontiguousarray(a, dtype=np.float64)).cuda()
+    with pytest.raises(hmpc.HmpcError, match='IndexError'):
+        cx.plan_device(d(x0[None]), d(xf[None]), cfg.N_run, cfg.N_k, cfg.dt, cfg.curve, cfg.t_p,
+                       cfg.phi_switch, cfg.t_start, 10 ** 6)
+    # the same context plans normally afterwards (the error word is per call)
+    x_ref, pf_ref, _ = cx.plan_device(d(x0[None]), d(xf[None]), cfg.N_run, cfg.N_k, cfg.dt, cfg.curve,
+                                      cfg.t_p, cfg.phi_switch, cfg.t_start, cfg.step_adjustment)
+    torch.cuda.synchronize()
+    assert np.isfinite(x_ref.cpu().numpy()).all()

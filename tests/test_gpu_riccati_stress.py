@@ -2,7 +2,11 @@
 batch sizes where the rare paths run: the cached-column z and its sweep
 fallback, drops, the overflow hand-off, both occupancy builds.
 
-Per case: equal statuses for every instance, |du| <= 1e-6 where solved.
+Per case: equal statuses for every instance and, where solved, |du| <= 1e-6,
+|dx*| <= 1e-6 (x* feeds the next mpcontrol call, src/mpc_cvx_euler_3f.py:58,68)
+and a relative objective error <= 1e-8.  x* is checked on its own: a sweep
+defect once corrupted x* of overflowed instances while u* stayed right
+(the DPP hazard).
 Workloads: the bench sampler with the mu sweep and start-state noise scaled
 up (x3 velocities, x2 rates) so that active sets are larger than the bench's."""
 import numpy as np
@@ -47,3 +51,6 @@ def test_riccati_stress_vs_port(hm, variant, N, B, curve, kernel):
     ok = ref['status'] == 0
     assert ok.mean() > 0.9
     assert np.abs(gpu['u'][ok] - ref['u'][ok]).max() <= 1e-6
+    assert np.abs(gpu['x'][ok] - ref['x'][ok]).max() <= 1e-6
+    rel = np.abs(gpu['obj'][ok] - ref['obj'][ok]) / np.maximum(np.abs(ref['obj'][ok]), 1.0)
+    assert rel.max() <= 1e-8, rel.max()

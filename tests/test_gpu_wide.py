@@ -47,6 +47,9 @@ def check(gpu, ref):
     dob = (np.abs(gpu['obj'][ok] - ref['obj'][ok]) / np.abs(ref['obj'][ok])).max(initial=0.0)
     assert du <= U_TOL, du
     assert dob <= OBJ_RTOL, dob
+    # x* too: it feeds the next mpcontrol call (src/mpc_cvx_euler_3f.py:58,68)
+    dx = np.abs(gpu['x'][ok] - ref['x'][ok]).max(initial=0.0)
+    assert dx <= U_TOL, dx
     return du
 
 
