@@ -19,8 +19,17 @@ for n in $HORIZONS; do LIST="$LIST X($n)"; done
 F32LIST=""
 for n in $F32_HORIZONS; do F32LIST="$F32LIST X($n)"; done
 pids=()
+# the split launch's compacted kernel (at most NV free variables, active-set
+# capacity Q, 3 waves / SIMD) per horizon: "N:NV:Q" (CMP="" disables)
+CMP=${CMP-"10:48:13"}
+cmp_flags() {
+  for e in $CMP; do
+    IFS=: read -r cn cv cq <<< "$e"
+    if [ "$cn" = "$1" ]; then echo "-DHMPC_CMP_NV=$cv -DHMPC_CMP_Q=$cq"; fi
+  done
+}
 for n in $HORIZONS; do
-  $HIPCC $FLAGS -DHMPC_INST_N=$n -c csrc/hmpc_kernels.hip -o $BDIR/hmpc_kernels_n$n.o "$@" &
+  $HIPCC $FLAGS -DHMPC_INST_N=$n $(cmp_flags $n) -c csrc/hmpc_kernels.hip -o $BDIR/hmpc_kernels_n$n.o "$@" &
   pids+=($!)
   while [ "$(jobs -rp | wc -l)" -ge "$JOBS" ]; do sleep 1; done
 done

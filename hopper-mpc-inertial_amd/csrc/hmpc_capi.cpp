@@ -33,14 +33,20 @@ struct hmpc_ctx {
   // generic-horizon kernel workspace (hmpc_wide.hip)
   double* wsbuf = nullptr;
   int wsgroups = 0;
-  // active-set overflow pass (hmpc_ric.hip): [count | list of ovf_cap ids]
-  // and the global R blocks of its workgroups
+  // active-set overflow pass (hmpc_ric.hip): [overflow count | Riccati
+  // instance counter | done counter | split counts (2) | pad (3) | list of
+  // ovf_cap ids] and the global R blocks of its workgroups
   int32_t* ovf = nullptr;
   int64_t ovf_cap = 0;
   // the counters need a zeroing before the next solve (fresh buffer, or a
   // solve whose overflow pass -- which zeroes them at its end -- did not run)
   bool ovf_dirty = true;
   double* rws = nullptr;
+  // dense split launch: the two class lists [2][split_cap]
+  int32_t* split = nullptr;
+  int64_t split_cap = 0;
+  hipStream_t split_stream = nullptr;   // the compacted class's stream
+  hipEvent_t split_fork = nullptr, split_join = nullptr;
   // Riccati kernel: per-workgroup K / Dinv workspace of its resident grid
   double* kws = nullptr;
   int ric_groups = 0;
@@ -89,6 +95,8 @@ hmpc::SolveArgs make_args(hmpc_ctx* c, int64_t B, const double* x_in, const doub
   a.ws = nullptr; a.ws_stride = 0; a.ws_groups = 0;
   a.ovf_count = nullptr; a.ovf_list = nullptr; a.rws = nullptr; a.rws_stride = 0;
   a.work = nullptr; a.kws = nullptr; a.kws_stride = 0; a.ric_groups = 0;
+  a.split_count = nullptr; a.split_list = nullptr; a.list = nullptr; a.list_count = nullptr;
+  a.split_stream = nullptr; a.split_fork = nullptr; a.split_join = nullptr;
   a.precision = c->precision;
   return a;
 }
@@ -135,6 +143,7 @@ int prepare_ric(hmpc_ctx* c, int64_t B, hmpc::SolveArgs& a) {
   const hmpc::Kernel k = hmpc::pick_kernel(c->variant, c->N, c->precision);
   a.ovf_count = nullptr; a.ovf_list = nullptr; a.rws = nullptr; a.rws_stride = 0;
   a.work = nullptr; a.kws = nullptr; a.kws_stride = 0; a.ric_groups = 0;
+  a.split_count = nullptr; a.split_list = nullptr;
   if (k == hmpc::Kernel::Cas) {   // instance counter + R slots, no overflow pass
     if (!c->ovf) {
       hipError_t e = hipMalloc(&c->ovf, sizeof(int32_t) * 4);
@@ -167,14 +176,40 @@ int prepare_ric(hmpc_ctx* c, int64_t B, hmpc::SolveArgs& a) {
     if (c->ovf) (void)hipFree(c->ovf);
     c->ovf = nullptr;
     c->ovf_cap = 0;
-    hipError_t e = hipMalloc(&c->ovf, sizeof(int32_t) * (size_t)(B + 4));
+    hipError_t e = hipMalloc(&c->ovf, sizeof(int32_t) * (size_t)(B + 8));
     if (e != hipSuccess) { c->err = "overflow list hipMalloc"; return HMPC_ERR_NOMEM; }
     c->ovf_cap = B;
     c->ovf_dirty = true;
   }
   a.ovf_count = c->ovf;
   a.work = c->ovf + 1;
-  a.ovf_list = c->ovf + 4;
+  a.ovf_list = c->ovf + 8;
+  // the dense kernel's split launch (compacted kernel for the instances with
+  // few free variables): class counts next to the overflow counters, which
+  // the overflow pass zeroes together at its end
+  if (k == hmpc::Kernel::Dense && hmpc::dense_split_nv(c->N, false) > 0) {
+    if (B > c->split_cap) {
+      if (c->split) (void)hipFree(c->split);
+      c->split = nullptr;
+      c->split_cap = 0;
+      hipError_t e = hipMalloc(&c->split, sizeof(int32_t) * 2 * (size_t)B);
+      if (e != hipSuccess) { c->err = "split list hipMalloc"; return HMPC_ERR_NOMEM; }
+      c->split_cap = B;
+    }
+    if (!c->split_stream) {
+      if (hipStreamCreateWithFlags(&c->split_stream, hipStreamNonBlocking) != hipSuccess ||
+          hipEventCreateWithFlags(&c->split_fork, hipEventDisableTiming) != hipSuccess ||
+          hipEventCreateWithFlags(&c->split_join, hipEventDisableTiming) != hipSuccess) {
+        c->err = "split stream / events";
+        return HMPC_ERR_HIP;
+      }
+    }
+    a.split_count = c->ovf + 3;
+    a.split_list = c->split;
+    a.split_stream = c->split_stream;
+    a.split_fork = c->split_fork;
+    a.split_join = c->split_join;
+  }
   a.rws = c->rws;
   a.rws_stride = rstride;
   if (k == hmpc::Kernel::Riccati) {
@@ -199,12 +234,13 @@ int run_solve(hmpc_ctx* c, hmpc::SolveArgs a, hipStream_t s) {
   if (rc != HMPC_OK) return rc;
   rc = prepare_ric(c, a.B, a);
   if (rc != HMPC_OK) return rc;
-  // [overflow count | instance counter | overflow-pass done counter]: zeroed
-  // here only when dirty -- the overflow pass, which follows every main pass
-  // that has one, zeroes them at its end (stream order: the next solve's
-  // kernels see them zero).  The CasADi kernel has no overflow pass.
+  // [overflow count | instance counter | overflow-pass done counter | split
+  // counts]: zeroed here only when dirty -- the overflow pass, which follows
+  // every main pass that has one, zeroes them at its end (stream order: the
+  // next solve's kernels see them zero).  The CasADi kernel has no overflow
+  // pass.
   if (a.work && (!a.ovf_count || c->ovf_dirty)) {
-    hipError_t e = hipMemsetAsync(a.work - 1, 0, 3 * sizeof(int32_t), s);
+    hipError_t e = hipMemsetAsync(a.work - 1, 0, (a.ovf_count ? 5 : 3) * sizeof(int32_t), s);
     if (e != hipSuccess) return fail_hip(c, e, "hipMemsetAsync(overflow count)");
   }
   c->ovf_dirty = true;   // until the overflow pass is launched
@@ -306,6 +342,10 @@ int hmpc_destroy(hmpc_ctx* c) {
   if (c->wsbuf) (void)hipFree(c->wsbuf);
   if (c->ovf) (void)hipFree(c->ovf);
   if (c->rws) (void)hipFree(c->rws);
+  if (c->split) (void)hipFree(c->split);
+  if (c->split_stream) (void)hipStreamDestroy(c->split_stream);
+  if (c->split_fork) (void)hipEventDestroy(c->split_fork);
+  if (c->split_join) (void)hipEventDestroy(c->split_join);
   if (c->kws) (void)hipFree(c->kws);
   if (c->plan_scratch) (void)hipFree(c->plan_scratch);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);

@@ -19,12 +19,14 @@ namespace hmpc {
 #define HMPC_DECL(n)                                                       \
   bool launch_solve_n##n(int variant, const SolveArgs& a, hipStream_t s); \
   int qmax_solve_n##n();                                                  \
+  int split_nv_n##n();                                                    \
   const char* name_solve_n##n(int variant);
 HMPC_HORIZON_LIST(HMPC_DECL)
 #undef HMPC_DECL
 #define HMPC_DECL(n)                                                           \
   bool launch_solve_n##n##_f32(int variant, const SolveArgs& a, hipStream_t s); \
   int qmax_solve_n##n##_f32();                                                  \
+  int split_nv_n##n##_f32();                                                    \
   const char* name_solve_n##n##_f32(int variant);
 HMPC_F32_LIST(HMPC_DECL)
 #undef HMPC_DECL
@@ -111,6 +113,21 @@ int dense_qmax(int N, bool f32) {
   HMPC_HORIZON_LIST(HMPC_CASE)
 #undef HMPC_CASE
   return -1;
+}
+
+int dense_split_nv(int N, bool f32) {
+  if (f32) {
+#define HMPC_CASE(n) \
+  if (N == n) return split_nv_n##n##_f32();
+    HMPC_F32_LIST(HMPC_CASE)
+#undef HMPC_CASE
+    return 0;
+  }
+#define HMPC_CASE(n) \
+  if (N == n) return split_nv_n##n();
+  HMPC_HORIZON_LIST(HMPC_CASE)
+#undef HMPC_CASE
+  return 0;
 }
 
 const char* dense_name(int variant, int N, bool f32) {

@@ -60,6 +60,20 @@ struct SolveArgs {
   int ric_groups;
   double* kws;
   int64_t kws_stride;
+  // Dense split launch (hmpc_kernels.hip, objects built with HMPC_CMP_NV):
+  // [compacted count | full count] (zero at the launch, zeroed again by the
+  // overflow pass at its end) and the two class lists [2][B]; nullptr = one
+  // launch of the full kernel.  list / list_count: set per launch by the
+  // launcher (the kernel's class list), nullptr = block i solves instance i.
+  int32_t* split_count;
+  int32_t* split_list;
+  const int32_t* list;
+  const int32_t* list_count;
+  // the split's second class runs concurrently on split_stream (forked from
+  // and joined back into the caller's stream by the two events); nullptr:
+  // both classes on the caller's stream, one after the other
+  hipStream_t split_stream;
+  hipEvent_t split_fork, split_join;
 };
 
 // The Riccati kernel (hmpc_ric.hip): any horizon 1 <= N <= kRicNmax, one
@@ -181,6 +195,8 @@ bool launch_solve_wide(int variant, int N, const SolveArgs& a, hipStream_t strea
 // the dedicated dense kernel's active-set capacity (-1: none) and name, as
 // its own object reports them (hmpc_kernels.hip)
 int dense_qmax(int N, bool f32);
+// free-variable bound of the dense split's compacted kernel (0: no split)
+int dense_split_nv(int N, bool f32);
 const char* dense_name(int variant, int N, bool f32);
 bool horizon_supported(int variant, int N);   // compiled, or generic (N <= kWideNmax)
 bool horizon_compiled(int variant, int N);    // a dedicated one-wavefront kernel

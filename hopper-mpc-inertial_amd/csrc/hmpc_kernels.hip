@@ -240,14 +240,19 @@ struct Blk {
 // ----------------------------------------------------------------------------
 // LDS layout (in doubles), one instance per workgroup
 // ----------------------------------------------------------------------------
-template <int N>
+// NVM > 0: the compacted kernel (one wave) for instances with at most NVM
+// free variables (hmpc_classify_kernel), NVM = 0: every instance (NV = 6N).
+// QM > 0 overrides the active-set capacity.
+template <int N, int NVM = 0, int QM = 0>
 struct Lay {
-  static constexpr int NV = 6 * N;
+  static constexpr int NVF = 6 * N;                 // the full input vector (outputs)
+  static constexpr int NV = NVM > 0 ? NVM : NVF;    // variables (lanes) of the factor
   static constexpr int W = (NV + 63) / 64;
   static constexpr int NT = 64 * W;
+  static_assert(W > 1 || NVF <= NT, "one-wave kernels keep the full vector in XS");
   // active-set capacity (registers for Qw, LDS for R); the largest active set
   // seen over 65536 random N=10 instances is 12
-  static constexpr int QMAX = NV < 20 ? NV : (N <= 10 ? 20 : 48);
+  static constexpr int QMAX = QM > 0 ? QM : (NV < 20 ? NV : (N <= 10 ? 20 : 48));
   static constexpr int e2(int n) { return (n + 1) & ~1; }
   static constexpr int NS = 22;                    // unique entries of S_t
   static constexpr int LCN = NV * (NV + 1) / 2;    // packed L
@@ -331,10 +336,9 @@ __device__ __forceinline__ void sweep_stage(real b, real& a0, real& a1, real* bu
 // multiple of 4): b is zero above row s0, so are the first s0 entries of y
 // and the sweep starts there (constraint normals are sparse: a box or
 // friction row of stage j starts at 6j).
-template <int N>
+template <class L>
 __device__ __forceinline__ real tri_fwd_lds(real acc, const real* Mc, const real* zero,
-                                              real dinv, real* red, int s0 = 0) {
-  using L = Lay<N>;
+                                              real dinv, real* red, int nf, int s0 = 0) {
   constexpr int NV = L::NV;
   constexpr int SEND = L::W == 1 ? (NV + 3) & ~3 : ((NV + kRing2 - 1) / kRing2) * kRing2;   // padded (steps >= NV are no-ops)
   const int tid = threadIdx.x;
@@ -343,8 +347,10 @@ __device__ __forceinline__ real tri_fwd_lds(real acc, const real* Mc, const real
     // (the lane mask is built on the scalar unit: no v_cmp per step)
     const unsigned base = lds_addr(Mc + tid), zaddr = lds_addr(zero);
     constexpr uint64_t kLive = NV >= 64 ? ~0ull : ((1ull << NV) - 1);
+    // (nf: the instance's free variables; steps >= nf are no-ops, their rows
+    // and columns are the identity)
     auto addr = [&](int s) -> unsigned {
-      const uint64_t m = s < NV ? kLive & ~((2ull << s) - 1) : 0;   // lanes s+1 .. NV-1
+      const uint64_t m = s < nf ? kLive & ~((2ull << s) - 1) : 0;   // lanes s+1 .. NV-1
       return msel(m, base + (unsigned)RB * (unsigned)(L::cb(s) - s), zaddr);
     };
     real ring[kRing1];
@@ -352,7 +358,7 @@ __device__ __forceinline__ real tri_fwd_lds(real acc, const real* Mc, const real
       lds_ld1(ring[decltype(jc)::value], addr(s0 + decltype(jc)::value));
     });
 #pragma unroll 1
-    for (int s = s0; s < NV; s += kRing1) {   // (steps >= NV are no-ops)
+    for (int s = s0; s < nf; s += kRing1) {   // (steps >= nf are no-ops)
       sfor<0, kRing1>([&](auto jc) __attribute__((always_inline)) {
         constexpr int j = decltype(jc)::value;
         const int sj = s + j;
@@ -409,12 +415,12 @@ __device__ __forceinline__ real tri_fwd_lds(real acc, const real* Mc, const real
 }
 // z = L^-T b (lane v holds b_v), M from the LDS copy.  One wave: loads of
 // step s-4 are issued at step s (a 4-deep ring of hand-counted loads).
-template <int N>
+template <class L>
 __device__ __forceinline__ real tri_bwd(real acc, const real* Mc, const real* zero,
-                                          real dinv, real* red) {
-  using L = Lay<N>;
+                                          real dinv, real* red, int nf) {
   constexpr int NV = L::NV;
-  constexpr int STOP = L::W == 1 ? ((NV + kRing1 - 1) & ~(kRing1 - 1)) - 1 : ((NV + 3) & ~3) - 1;   // first step, padded (steps >= NV are no-ops)
+  // first step, padded to the ring (steps >= nf are no-ops)
+  const int STOP = L::W == 1 ? ((nf + kRing1 - 1) & ~(kRing1 - 1)) - 1 : ((NV + 3) & ~3) - 1;
   const int tid = threadIdx.x;
   const int cbt = tid < NV ? L::cb(tid) : 0;
   acc *= dinv;
@@ -423,7 +429,7 @@ __device__ __forceinline__ real tri_bwd(real acc, const real* Mc, const real* ze
     // (the lane mask is built on the scalar unit: no v_cmp per step)
     const unsigned base = lds_addr(Mc + cbt - tid), zaddr = lds_addr(zero);
     auto addr = [&](int s) -> unsigned {
-      const uint64_t m = (s > 0 && s < NV) ? (1ull << s) - 1 : 0;   // lanes 0 .. s-1
+      const uint64_t m = (s > 0 && s < nf) ? (1ull << s) - 1 : 0;   // lanes 0 .. s-1
       return msel(m, base + (unsigned)RB * (unsigned)s, zaddr);
     };
     real ring[kRing1];
@@ -506,6 +512,13 @@ __device__ __forceinline__ real tri_bwd(real acc, const real* Mc, const real* ze
 #define HMPC_TOC(slot, v) ((void)0)
 #endif
 
+// skip the Cholesky update FMAs of the padding columns (>= nf) chunk by
+// chunk (1), or update every column (0)
+#ifndef HMPC_CHUNK_SKIP
+#define HMPC_CHUNK_SKIP 0
+#endif
+constexpr bool kSkipChunks = HMPC_CHUNK_SKIP;
+
 // issue priority of the chain-bound phases: 0 off, 1 (default) the Cholesky
 // through the active set, 2 the Cholesky only.  A wave in its dependent
 // pivot/sweep chains issues first; the co-resident wave's throughput phases
@@ -516,11 +529,17 @@ __device__ __forceinline__ real tri_bwd(real acc, const real* Mc, const real* ze
 #ifndef HMPC_WAVES_PER_EU
 #define HMPC_WAVES_PER_EU(W) ((W) == 1 ? 2 : 1)
 #endif
-template <int VAR, int N, typename R>
-__global__ void __launch_bounds__(Lay<N>::NT, HMPC_WAVES_PER_EU(Lay<N>::W))
+// waves / SIMD of the compacted kernel (NVM > 0)
+#ifndef HMPC_CMP_WAVES
+#define HMPC_CMP_WAVES 3
+#endif
+template <int VAR, int N, typename R, int NVM = 0, int QM = 0>
+__global__ void __launch_bounds__((Lay<N, NVM, QM>::NT),
+                                  (NVM > 0 ? HMPC_CMP_WAVES : HMPC_WAVES_PER_EU((Lay<N, NVM, QM>::W))))
 solve_kernel(SolveArgs a) {
   static_assert(sizeof(R) == sizeof(real), "one arithmetic type per build");
-  using L = Lay<N>;
+  using L = Lay<N, NVM, QM>;
+  static_assert(NVM == 0 || L::W == 1, "the compacted kernel is one wave");
   constexpr int NV = L::NV;
   constexpr int W = L::W;
   constexpr int NT = L::NT;
@@ -535,7 +554,13 @@ solve_kernel(SolveArgs a) {
   HMPC_STAMP(0);
 
   const int tid = threadIdx.x;
-  const int64_t b = blockIdx.x;
+  // split launch (launch_solve_n<N>): block i solves the i-th instance of this
+  // kernel's class list; blocks beyond the list's length have no work
+  int64_t b = blockIdx.x;
+  if (a.list) {
+    if ((int)blockIdx.x >= *a.list_count) return;
+    b = a.list[blockIdx.x];
+  }
   const real dt = a.dt;
   const real dtm = dt / real(a.m);
 
@@ -776,13 +801,52 @@ solve_kernel(SolveArgs a) {
   HMPC_STAMP(3);
 
   // ---------------- phase 3: Hessian row (lower part) + gradient ------------
-  const int vj3 = tid / 6, vc3 = tid - 6 * (tid / 6);   // stage / component of my variable
-  const bool active_lane = tid < NV;
+  // Variable map.  One wave (W == 1): the FREE variables only, compacted in
+  // stage order -- stage j holds its stance forces (3f fx fy fz, 2f fx fz;
+  // none when it swings) and then its three torques -- nf <= NV of them.
+  // Lane v owns compacted variable v = (stage vj, component vc); lanes >= nf
+  // are padding (identity rows, no constraints).  The fixed variables (swing
+  // forces :134-136, 2f fy 2f :129) are not in the factor at all, so swing
+  // windows factor, sweep and search a smaller problem.  Two waves: lane v
+  // owns variable 6 vj + vc and fixed variables are identity rows in place.
+  constexpr int KF = VAR == 3 ? 3 : 2;   // free forces of a stance stage
   const real ubar_z_alias = (sm[L::CC + N - 1] != 0.0) ? 2.0 * a.m * a.g : 0.0;
   auto is_fixed = [&](int k, int c) -> bool {   // swing f = 0 (:134-136), 2f fy = 0 (2f :129)
     return (c < 3 && sm[L::CC + k] == 0.0) || (VAR == 2 && c == 1);
   };
-  const bool my_fixed = active_lane && is_fixed(vj3, vc3);
+  // stance stages as a wave-uniform bit mask (one wave)
+  const uint64_t smask = __ballot(tid < N && sm[L::CC + (tid < N ? tid : 0)] != 0.0);
+  // first compacted variable of stage j (uniform)
+  auto stage_off = [&](int j) -> int {
+    return 3 * j + KF * __builtin_popcountll(smask & ((1ull << j) - 1));
+  };
+  const int nf = W == 1 ? uni(3 * N + KF * __builtin_popcountll(smask)) : NV;
+  // stage / component of lane t's compacted variable (W == 1)
+  auto vmap = [&](int t, int& vj, int& vc) __attribute__((always_inline)) {
+    vj = 0;
+    vc = 3;
+    sfor<0, N>([&](auto jc) __attribute__((always_inline)) {
+      constexpr int j = decltype(jc)::value;
+      const bool st = (smask >> j) & 1;
+      const int r = t - stage_off(j);
+      const int cs = st ? (VAR == 3 ? r : (r == 0 ? 0 : r + 1)) : r + 3;
+      const bool in = r >= 0 && r < (st ? 3 + KF : 3);
+      vj = in ? j : vj;
+      vc = in ? cs : vc;
+    });
+  };
+  int vj3, vc3;
+  bool active_lane, my_fixed;   // owns a variable of the factor; an identity row
+  if constexpr (W == 1) {
+    vmap(tid, vj3, vc3);
+    active_lane = tid < nf;
+    my_fixed = !active_lane;
+  } else {
+    vj3 = tid / 6;
+    vc3 = tid - 6 * (tid / 6);
+    active_lane = tid < NV;
+    my_fixed = active_lane && is_fixed(vj3, vc3);
+  }
 
   real Rg[NV];   // row `tid` of H (lower part), then the Cholesky trailing row
   real hv = 0.0;
@@ -815,9 +879,8 @@ solve_kernel(SolveArgs a) {
     real g[12];
 #pragma unroll
     for (int r = 0; r < 12; ++r) g[r] = f[r];
-    sfor<0, N>([&](auto jc) __attribute__((always_inline)) {
-      constexpr int j = N - 1 - decltype(jc)::value;
-      const real* smj = sm + opaque_zero();   // keeps this step's loads here
+    auto advance = [&](auto jc, const real* smj) __attribute__((always_inline)) {   // g -> g_j
+      constexpr int j = decltype(jc)::value;
       if constexpr (j < N - 1) {
         const real cp1 = smj[L::CS + 2 * (j + 1)], sp1 = smj[L::CS + 2 * (j + 1) + 1];
         real gn[12];
@@ -827,21 +890,73 @@ solve_kernel(SolveArgs a) {
 #pragma unroll
         for (int r = 0; r < 12; ++r) g[r] = (ii > j) ? gn[r] : g[r];
       }
-      const real cp = smj[L::CS + 2 * j], sp = smj[L::CS + 2 * j + 1];
-      const real* bw = smj + L::BW + 18 * j;
-      // fixed columns (swing forces :134-136) of stage j: zero
-      const real stance_j = smj[L::CC + j] != 0.0 ? 1.0 : 0.0;
-      sfor<0, 6>([&](auto c2c) __attribute__((always_inline)) {
-        constexpr int c2 = decltype(c2c)::value;
-        constexpr int w = 6 * j + c2;
-        real val;
-        if constexpr (VAR == 2 && c2 == 1) val = 0.0;   // 2f fy (2f :129)
-        else if constexpr (c2 < 3) val = stance_j * bd_dot<VAR>(c2, g, bw, dtm, cp, sp);
-        else val = bd_dot<VAR>(c2, g, bw, dtm, cp, sp);
-        Rg[w] = val;
-        pin(Rg[w]);
+    };
+    if constexpr (W == 1) {
+      // The compacted column index of (j, c2) is wave-uniform but not known
+      // at compile time, and registers cannot be indexed at run time: each
+      // lane writes its row into a packed lower-triangular image of H in LDS
+      // (row v at v(v+1)/2, over the dead union A: S and the adjoint are in
+      // registers by now), then reads it back by compile-time column.
+      // Entries right of the diagonal are not written (a per-lane scratch
+      // slot in the column buffers takes them); padding lanes read a zero
+      // row (XS, zeroed here).
+      real* hp = sm + L::LC;
+      const unsigned rowa = lds_addr(hp + ((tid * (tid + 1)) >> 1));
+      const unsigned dumpa = lds_addr(sm + L::COLB + tid);
+      xs[tid] = 0.0;
+      B::sync();   // every lane's S / adjoint reads are issued before the first H store
+      sfor<0, N>([&](auto jc) __attribute__((always_inline)) {
+        constexpr int j = N - 1 - decltype(jc)::value;
+        const real* smj = sm + opaque_zero();   // keeps this step's loads here
+        advance(std::integral_constant<int, j>{}, smj);
+        const real cp = smj[L::CS + 2 * j], sp = smj[L::CS + 2 * j + 1];
+        const real* bw = smj + L::BW + 18 * j;
+        const bool st = (smask >> j) & 1;   // uniform
+        const int o = stage_off(j);
+        auto put = [&](int w, real val) __attribute__((always_inline)) {
+          const unsigned ad = (w <= tid && active_lane) ? rowa + (unsigned)RB * (unsigned)w : dumpa;
+          *(lds_real*)ad = val;
+        };
+        if (st) {   // the stance forces (2f: fx, fz)
+          sfor<0, 3>([&](auto c2c) __attribute__((always_inline)) {
+            constexpr int c2 = decltype(c2c)::value;
+            if constexpr (!(VAR == 2 && c2 == 1))
+              put(o + (VAR == 3 ? c2 : (c2 == 0 ? 0 : 1)), bd_dot<VAR>(c2, g, bw, dtm, cp, sp));
+          });
+        }
+        const int ot = o + (st ? KF : 0);   // the torques
+        sfor<3, 6>([&](auto c2c) __attribute__((always_inline)) {
+          constexpr int c2 = decltype(c2c)::value;
+          put(ot + c2 - 3, bd_dot<VAR>(c2, g, bw, dtm, cp, sp));
+        });
       });
-    });
+      B::sync();
+      const real* row = active_lane ? hp + ((tid * (tid + 1)) >> 1) : xs;
+      sfor<0, NV>([&](auto wc) __attribute__((always_inline)) {
+        constexpr int w = decltype(wc)::value;
+        Rg[w] = row[w];
+      });
+    } else {
+      sfor<0, N>([&](auto jc) __attribute__((always_inline)) {
+        constexpr int j = N - 1 - decltype(jc)::value;
+        const real* smj = sm + opaque_zero();   // keeps this step's loads here
+        advance(std::integral_constant<int, j>{}, smj);
+        const real cp = smj[L::CS + 2 * j], sp = smj[L::CS + 2 * j + 1];
+        const real* bw = smj + L::BW + 18 * j;
+        // fixed columns (swing forces :134-136) of stage j: zero
+        const real stance_j = smj[L::CC + j] != 0.0 ? 1.0 : 0.0;
+        sfor<0, 6>([&](auto c2c) __attribute__((always_inline)) {
+          constexpr int c2 = decltype(c2c)::value;
+          constexpr int w = 6 * j + c2;
+          real val;
+          if constexpr (VAR == 2 && c2 == 1) val = 0.0;   // 2f fy (2f :129)
+          else if constexpr (c2 < 3) val = stance_j * bd_dot<VAR>(c2, g, bw, dtm, cp, sp);
+          else val = bd_dot<VAR>(c2, g, bw, dtm, cp, sp);
+          Rg[w] = val;
+          pin(Rg[w]);
+        });
+      });
+    }
     if (active_lane && !my_fixed) {
       real ub = 0.0;
       if (vc3 == 2) ub = a.uref_aliased ? ubar_z_alias : ((sm[L::CC + vj3] != 0.0) ? 2.0 * a.m * a.g : 0.0);
@@ -858,8 +973,8 @@ solve_kernel(SolveArgs a) {
   real dinv = 0.0;
   // the diagonal of H not built in phase 3: 1 for a fixed variable (identity
   // row/column), else 2 V_i (R * kuf: every stage but the last, 3f :114,132,139)
-  auto diag_extra = [&](int k, bool fixed) -> real {
-    return fixed ? 1.0 : ((k / 6 != N - 1) ? 2.0 * kRdiag : 0.0);
+  auto diag_extra = [&](int stage, bool fixed) -> real {
+    return fixed ? 1.0 : ((stage != N - 1) ? 2.0 * kRdiag : 0.0);
   };
 
   // ---------------- phase 4: Cholesky ---------------------------------------
@@ -896,8 +1011,7 @@ solve_kernel(SolveArgs a) {
         return (NV - ja - CW * ch) >= CW ? CW / 2
                                          : ((NV - ja - CW * ch) > 0 ? (NV - ja - CW * ch + 1) / 2 : 0);
       };
-      const uint64_t fixmask = __ballot(active_lane && is_fixed(vj3, vc3));
-      const real dx = diag_extra(tid, my_fixed);   // lane s: the extra of pivot s
+      const real dx = diag_extra(vj3, my_fixed);   // lane s: the extra of pivot s
       real2 nb[CW / 2];                 // chunk 0 of the next step
       real p_rs = 0.0, p_tk = 0.0;   // next step's 1/L_kk and M[tid][k]
       // the two column buffers' LDS addresses, held in registers (opaque):
@@ -931,13 +1045,13 @@ solve_kernel(SolveArgs a) {
       ahead(std::integral_constant<int, 0>{});
       constexpr uint64_t kLive = NV >= 64 ? ~0ull : ((1ull << NV) - 1);
       const unsigned tb = lds_addr(sm + tid);
-      sfor<0, NV>([&](auto kc) __attribute__((always_inline)) {
+      // steps 0 .. nf-1 only: the compacted factor has no fixed variables,
+      // and the padding rows beyond nf are the identity (never stepped)
+      ladder<0, NV>(nf, [&](auto kc) __attribute__((always_inline)) {
         constexpr int k = decltype(kc)::value;
         constexpr int JA = (k + 1) & ~1;   // 16-B aligned start of the update
         constexpr int NCH = (NV - JA + CW - 1) / CW;
         constexpr int NAHEAD = (k + 1 < NV) ? 1 + nldc((k + 2) & ~1, 0) : 0;   // LDS ops of ahead()
-        constexpr bool kfixed = VAR == 2 && k % 6 == 1;                       // 2f fy
-        constexpr bool kforce = k % 6 < 3;
         const real rs = p_rs, tk = p_tk;
         lds_wait<0>(nb[0], nb[1]);   // this step's chunk 0 (and everything older)
         // every lane updates: a lane <= k changes only its registers > k, the
@@ -988,31 +1102,30 @@ solve_kernel(SolveArgs a) {
             }
           });
         };
-        if constexpr (!kfixed) {
-          const bool run = !kforce || !((fixmask >> k) & 1);   // uniform
-          if (run) {
-            load(std::integral_constant<int, 1>{});
-            load(std::integral_constant<int, 2>{});
-            if constexpr (NCH > 0) update(std::integral_constant<int, 0>{}, nb);
-          }
-          if constexpr (k + 1 < NV) ahead(std::integral_constant<int, k + 1>{});
-          if (run) {
-            sfor<1, NCH>([&](auto chc) __attribute__((always_inline)) {
-              constexpr int ch = decltype(chc)::value;
-              load(std::integral_constant<int, ch + 2>{});
-              // LDS ops issued after chunk ch's loads (issue order: chunks 1,
-              // 2, ahead(), then chunk c+2 at iteration c)
-              constexpr int younger = ch == 1 ? nl(JA, 2) + NAHEAD + nl(JA, 3)
-                                    : ch == 2 ? NAHEAD + nl(JA, 3) + nl(JA, 4)
-                                              : nl(JA, ch + 1) + nl(JA, ch + 2);
-              lds_wait<younger>(buf[ch % 3][0], buf[ch % 3][1]);
-              update(chc, buf[ch % 3]);
-            });
-          }
-        } else {
-          if constexpr (k + 1 < NV) ahead(std::integral_constant<int, k + 1>{});
+        // chunks holding columns < nf (uniform; k < nf so JA <= nf): the
+        // FMAs of the chunks beyond (padding columns) are skipped; their
+        // loads still issue, so every wait keeps its compile-time count
+        const int nchr = (nf - JA + CW - 1) / CW;
+        load(std::integral_constant<int, 1>{});
+        load(std::integral_constant<int, 2>{});
+        if constexpr (NCH > 0) {
+          if (!kSkipChunks || nchr > 0) update(std::integral_constant<int, 0>{}, nb);
         }
+        if constexpr (k + 1 < NV) ahead(std::integral_constant<int, k + 1>{});
+        sfor<1, NCH>([&](auto chc) __attribute__((always_inline)) {
+          constexpr int ch = decltype(chc)::value;
+          load(std::integral_constant<int, ch + 2>{});
+          // LDS ops issued after chunk ch's loads (issue order: chunks 1,
+          // 2, ahead(), then chunk c+2 at iteration c)
+          constexpr int younger = ch == 1 ? nl(JA, 2) + NAHEAD + nl(JA, 3)
+                                : ch == 2 ? NAHEAD + nl(JA, 3) + nl(JA, 4)
+                                          : nl(JA, ch + 1) + nl(JA, ch + 2);
+          lds_wait<younger>(buf[ch % 3][0], buf[ch % 3][1]);
+          if (!kSkipChunks || ch < nchr) update(chc, buf[ch % 3]);
+        });
       });
+      // the last step's lookahead loaded a padding column: drain it
+      lds_wait<0>(nb[0], nb[1]);
     } else {
       real mine = Rg[0];   // A[tid][k] of the current step
       // pivot extras (diag_extra) by lane, behind the column buffers (the
@@ -1020,7 +1133,7 @@ solve_kernel(SolveArgs a) {
       // publishes them
       real* dxa = sm + L::COLB + 2 * (NT + 8);
       static_assert(L::COLB + 2 * (NT + 8) + NT <= L::U0, "pivot extras do not fit");
-      dxa[tid] = diag_extra(tid, my_fixed);
+      dxa[tid] = diag_extra(vj3, my_fixed);
       sfor<0, (NV + 7) / 8>([&](auto bc) __attribute__((always_inline)) {
         constexpr int bb = decltype(bc)::value;
         constexpr int J0 = 8 * bb;
@@ -1087,6 +1200,7 @@ solve_kernel(SolveArgs a) {
     __syncthreads();
     if (nbad != 0.0 || okall == 0) status = ST_NUMERICAL;
     dinv = tid < NV ? sm[L::LC + L::cb(tid < NV ? tid : 0)] : 0.0;   // 1 / L[tid][tid]
+    if constexpr (W == 1) dinv = active_lane ? dinv : real(1);   // padding: never stepped
   }
   HMPC_STAMP(5);
   if constexpr (HMPC_PRIO == 2) __builtin_amdgcn_s_setprio(0);
@@ -1099,7 +1213,7 @@ solve_kernel(SolveArgs a) {
   {
     real y;
     y = wv * dinv;   // L^-1 (-h), swept during the Cholesky
-    v = tri_bwd<N>(y, Lc, zero, dinv, xs);
+    v = tri_bwd<L>(y, Lc, zero, dinv, xs, nf);
   }
   HMPC_STAMP(6);
 
@@ -1110,8 +1224,16 @@ solve_kernel(SolveArgs a) {
   // stage / component of my variable, recomputed from an opaque thread id:
   // phase 3's copies would stay alive (spilled) across the factorisation
   const int tid_o = tid + opaque_zero();
-  const int vj = (tid_o * 43) >> 8;   // tid / 6 for tid < 128
-  const int vc = tid_o - 6 * vj;
+  int vj, vc;
+  if constexpr (W == 1) {
+    vmap(tid_o, vj, vc);
+    active_lane = tid_o < nf;
+  } else {
+    vj = (tid_o * 43) >> 8;   // tid / 6 for tid < 128
+    vc = tid_o - 6 * vj;
+  }
+  // the full-order slot of my variable in XS (padding lanes: a spare slot)
+  const int fidx = W == 1 ? (active_lane ? 6 * vj + vc : NT - 1) : tid_o;
 
   // ---------------- phase 6: Goldfarb-Idnani, range-space form --------------
   // Constraints owned by lane v (id = 4 v + slot), all as n'v >= b:
@@ -1170,24 +1292,37 @@ solve_kernel(SolveArgs a) {
   const int max_iter = 4 * NV + 50;
 
   // coefficient of lane `i`'s variable in constraint `id`, and its rhs
-  auto coef_of = [&](int id, int i) -> real {
-    const int o = id >> 2, sl = id & 3, oj = o / 6, oc = o - 6 * oj;
-    if (i >= NV) return 0.0;
+  // (stage, component) of the variable of lane o (uniform o)
+  auto owner = [&](int o, int& oj, int& oc) __attribute__((always_inline)) {
+    if constexpr (W == 1) {
+      oj = __builtin_amdgcn_readlane(vj, o);
+      oc = __builtin_amdgcn_readlane(vc, o);
+    } else {
+      oj = o / 6;
+      oc = o - 6 * oj;
+    }
+  };
+  auto coef_of = [&](int id, int i) -> real {   // (i: this lane)
+    const int o = id >> 2, sl = id & 3;
+    int oj, oc;
+    owner(o, oj, oc);
+    if (!active_lane) return 0.0;
     if (oc >= 3) {
       if (sl == 0) return i == o ? 1.0 : 0.0;
       if (sl == 1) return i == o ? -1.0 : 0.0;
       // z-row of stage oj over fz_j, j <= oj-2
-      const int ij = i / 6, ic = i - 6 * ij;
-      if (ic != 2 || ij > oj - 2 || sm[L::CC + ij] == 0.0) return 0.0;
-      return zc * (real)(oj - 1 - ij);
+      if (vc != 2 || vj > oj - 2 || sm[L::CC + vj] == 0.0) return 0.0;
+      return zc * (real)(oj - 1 - vj);
     }
     if (oc == 2) return i == o ? (sl == 0 ? 1.0 : -1.0) : 0.0;
     if (i == o) return sl == 0 ? -1.0 : 1.0;
-    if (i == 6 * oj + 2) return mu;
+    if (vj == oj && vc == 2) return mu;
     return 0.0;
   };
   auto rhs_of = [&](int id) -> real {
-    const int o = id >> 2, sl = id & 3, oj = o / 6, oc = o - 6 * oj;
+    const int o = id >> 2, sl = id & 3;
+    int oj, oc;
+    owner(o, oj, oc);
     if (oc >= 3) {
       if (sl < 2) return -tau_lim(oc);
       return real(kZmin) - sm[L::ZB + oj];
@@ -1200,7 +1335,7 @@ solve_kernel(SolveArgs a) {
   while (!done) {
     // ---- slacks of my constraints; pick the most violated ----
     HMPC_TIC(t_scan);
-    xs[tid] = v;
+    xs[fidx] = v;   // full order (fixed variables: 0)
     B::sync();
     // branch-free: slots 0/1 are +-a0 v + muf fz_stage + k0/k1; slot 2 the
     // z row ZB_k + zc ((k-1) S1 - S2) with S1 = sum C_j fz_j, S2 = sum j C_j fz_j
@@ -1233,7 +1368,7 @@ solve_kernel(SolveArgs a) {
     // w = L^-1 n_p
     HMPC_TIC(t_fwd);
     const int s0 = B::first(np_me != 0.0, red);   // first nonzero of n_p (-1: none)
-    const real wfull = tri_fwd_lds<N>(np_me, Lc, zero, dinv, xs, s0 > 0 ? (s0 & ~(W == 1 ? 3 : kRing2 - 1)) : 0);
+    const real wfull = tri_fwd_lds<L>(np_me, Lc, zero, dinv, xs, nf, s0 > 0 ? (s0 & ~(W == 1 ? 3 : kRing2 - 1)) : 0);
     const real wnorm2 = B::sum(wfull * wfull, red);
     HMPC_TOC(10, t_fwd);
 
@@ -1278,7 +1413,7 @@ solve_kernel(SolveArgs a) {
       HMPC_TOC(11, t_gs);
       // primal direction z = L^-T w_perp (lane v gets z_v)
       HMPC_TIC(t_bwd);
-      const real zi = tri_bwd<N>(wp, Lc, zero, dinv, xs);
+      const real zi = tri_bwd<L>(wp, Lc, zero, dinv, xs, nf);
       HMPC_TOC(12, t_bwd);
       HMPC_TIC(t_dual);
       // dual direction r = R^-1 c (lanes l < q), back substitution
@@ -1409,9 +1544,9 @@ solve_kernel(SolveArgs a) {
     constexpr int k = decltype(kc)::value;
     xrg[k] = xrf7[k * xrs + (tid < 12 ? tid : 0)];
   });
-  if (active_lane) a.u[b * NV + tid] = v;
-  xs[tid] = v;
+  xs[fidx] = v;   // full order (fixed variables: 0)
   __syncthreads();   // L is dead: XO aliases it
+  if (tid < L::NVF) a.u[b * L::NVF + tid] = xs[tid];
   {
     real* xo = sm + L::XO;
     real xr = tid < 12 ? sm[L::XIN + tid] : 0.0;
@@ -1474,6 +1609,39 @@ solve_kernel(SolveArgs a) {
   }
 }
 
+// Split launch: each instance goes to the compacted one-wave kernel (at most
+// NVM free variables: NVM-wide rows, 3 waves / SIMD) or to the full kernel,
+// by the number of stance stages of its contact schedule C (free variables
+// nf = 3N + (3f: 3, 2f: 2) x stance stages).  One thread per instance; the
+// two class lists are appended wave by wave (one atomic per wave and list):
+// list A at split_list[0..B), list B at split_list[B..2B), lengths in
+// split_count[0..1] (zero at the launch; the overflow pass zeroes them).
+template <int VAR, int N, int NVM>
+__global__ void __launch_bounds__(256) classify_kernel(SolveArgs a) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const bool in = i < a.B;
+  int nst = 0;
+  if (in) {
+    const double* c = a.C + i * a.C_bs;
+#pragma unroll
+    for (int k = 0; k < N; ++k) nst += c[k] != 0.0 ? 1 : 0;
+  }
+  const int nf = 3 * N + (VAR == 3 ? 3 : 2) * nst;
+  const bool cmp = in && nf <= NVM, full = in && !cmp;
+  const uint64_t mc = __ballot(cmp), mf = __ballot(full);
+  const int lane = threadIdx.x & 63;
+  const uint64_t lt = (1ull << lane) - 1;
+  int bc = 0, bf = 0;
+  if (lane == 0) {
+    if (mc) bc = atomicAdd(a.split_count, __builtin_popcountll(mc));
+    if (mf) bf = atomicAdd(a.split_count + 1, __builtin_popcountll(mf));
+  }
+  bc = __builtin_amdgcn_readfirstlane(bc);
+  bf = __builtin_amdgcn_readfirstlane(bf);
+  if (cmp) a.split_list[bc + __builtin_popcountll(mc & lt)] = (int32_t)i;
+  if (full) a.split_list[a.B + bf + __builtin_popcountll(mf & lt)] = (int32_t)i;
+}
+
 }  // namespace
 
 // ----------------------------------------------------------------------------
@@ -1495,25 +1663,72 @@ bool HMPC_CAT(HMPC_CAT(launch_solve_n, HMPC_INST_N), HMPC_LAUNCH_SUFFIX)(int var
   constexpr int N = HMPC_INST_N;
   constexpr int NT = Lay<N>::NT;
   if (a.B <= 0) return true;
-  if (variant == 3) {
-    hipLaunchKernelGGL((solve_kernel<3, N, real>), dim3((unsigned)a.B), dim3(NT), 0, s, a);
+  if (variant != 2 && variant != 3) return false;
+  SolveArgs af = a;
+  af.list = nullptr;
+  af.list_count = nullptr;
+#if defined(HMPC_CMP_NV) && HMPC_CMP_NV > 0
+  if (a.split_list && a.split_count) {   // classify, then one launch per class
+    const unsigned cb = (unsigned)((a.B + 255) / 256);
+    SolveArgs ac = af;
+    ac.list = a.split_list;
+    ac.list_count = a.split_count;
+    af.list = a.split_list + a.B;
+    af.list_count = a.split_count + 1;
+    if (variant == 3) hipLaunchKernelGGL((classify_kernel<3, N, HMPC_CMP_NV>), dim3(cb), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((classify_kernel<2, N, HMPC_CMP_NV>), dim3(cb), dim3(256), 0, s, a);
+    // the two classes run concurrently: the full kernel on the caller's
+    // stream, the compacted one on the split stream, joined back before the
+    // overflow pass (one kernel's tail fills with the other's waves)
+    hipStream_t s2 = s;
+    if (a.split_stream && a.split_fork && a.split_join) {
+      if (hipEventRecord(a.split_fork, s) != hipSuccess) return false;
+      if (hipStreamWaitEvent(a.split_stream, a.split_fork, 0) != hipSuccess) return false;
+      s2 = a.split_stream;
+    }
+    if (variant == 3) hipLaunchKernelGGL((solve_kernel<3, N, real>), dim3((unsigned)a.B), dim3(NT), 0, s, af);
+    else hipLaunchKernelGGL((solve_kernel<2, N, real>), dim3((unsigned)a.B), dim3(NT), 0, s, af);
+    if (variant == 3)
+      hipLaunchKernelGGL((solve_kernel<3, N, real, HMPC_CMP_NV, HMPC_CMP_Q>), dim3((unsigned)a.B), dim3(64), 0, s2, ac);
+    else
+      hipLaunchKernelGGL((solve_kernel<2, N, real, HMPC_CMP_NV, HMPC_CMP_Q>), dim3((unsigned)a.B), dim3(64), 0, s2, ac);
+    if (s2 != s) {
+      if (hipEventRecord(a.split_join, s2) != hipSuccess) return false;
+      if (hipStreamWaitEvent(s, a.split_join, 0) != hipSuccess) return false;
+    }
     return true;
   }
-  if (variant == 2) {
-    hipLaunchKernelGGL((solve_kernel<2, N, real>), dim3((unsigned)a.B), dim3(NT), 0, s, a);
-    return true;
-  }
-  return false;
+#endif
+  if (variant == 3) hipLaunchKernelGGL((solve_kernel<3, N, real>), dim3((unsigned)a.B), dim3(NT), 0, s, af);
+  else hipLaunchKernelGGL((solve_kernel<2, N, real>), dim3((unsigned)a.B), dim3(NT), 0, s, af);
+  return true;
 }
+
 // this object's active-set capacity and kernel names (hmpc_active_capacity,
 // hmpc_kernel_name: read from here, not restated in the C API)
 #define HMPC_STR2(x) #x
 #define HMPC_STR(x) HMPC_STR2(x)
-int HMPC_CAT(HMPC_CAT(qmax_solve_n, HMPC_INST_N), HMPC_LAUNCH_SUFFIX)() { return Lay<HMPC_INST_N>::QMAX; }
+// (the split's compacted kernel: its capacity when smaller; the names of both)
+#if defined(HMPC_CMP_NV) && HMPC_CMP_NV > 0
+#define HMPC_SPLIT_NV HMPC_CMP_NV
+#define HMPC_NAME_CMP(v) "hmpc::solve_kernel<" #v ", " HMPC_STR(HMPC_INST_N) ", " HMPC_STR(HMPC_REAL) ", " \
+  HMPC_STR(HMPC_CMP_NV) ", " HMPC_STR(HMPC_CMP_Q) "> + "
+constexpr int kCapCmp = Lay<HMPC_INST_N, HMPC_CMP_NV, HMPC_CMP_Q>::QMAX;
+#else
+#define HMPC_SPLIT_NV 0
+#define HMPC_NAME_CMP(v) ""
+constexpr int kCapCmp = 1 << 30;
+#endif
+int HMPC_CAT(HMPC_CAT(qmax_solve_n, HMPC_INST_N), HMPC_LAUNCH_SUFFIX)() {
+  return Lay<HMPC_INST_N>::QMAX < kCapCmp ? Lay<HMPC_INST_N>::QMAX : kCapCmp;
+}
+int HMPC_CAT(HMPC_CAT(split_nv_n, HMPC_INST_N), HMPC_LAUNCH_SUFFIX)() { return HMPC_SPLIT_NV; }
 const char* HMPC_CAT(HMPC_CAT(name_solve_n, HMPC_INST_N), HMPC_LAUNCH_SUFFIX)(int variant) {
   // (the template arguments as rocprofv3 demangles them)
-  if (variant == 3) return "hmpc::solve_kernel<3, " HMPC_STR(HMPC_INST_N) ", " HMPC_STR(HMPC_REAL) ">";
-  if (variant == 2) return "hmpc::solve_kernel<2, " HMPC_STR(HMPC_INST_N) ", " HMPC_STR(HMPC_REAL) ">";
+  if (variant == 3)
+    return HMPC_NAME_CMP(3) "hmpc::solve_kernel<3, " HMPC_STR(HMPC_INST_N) ", " HMPC_STR(HMPC_REAL) ", 0, 0>";
+  if (variant == 2)
+    return HMPC_NAME_CMP(2) "hmpc::solve_kernel<2, " HMPC_STR(HMPC_INST_N) ", " HMPC_STR(HMPC_REAL) ", 0, 0>";
   return "";
 }
 

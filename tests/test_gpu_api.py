@@ -63,21 +63,22 @@ def test_bad_tensors_raise(hm):
 
 
 def test_kernel_names(hm):
-    assert make(hm, 10).kernel_name == 'hmpc::solve_kernel<3, 10, double>'
+    assert make(hm, 10).kernel_name == 'hmpc::solve_kernel<3, 10, double, 48, 13> + hmpc::solve_kernel<3, 10, double, 0, 0>'
     assert make(hm, 20).kernel_name == 'hmpc::ric_kernel<3, 2, 0, 0>'   # 2 waves / SIMD
     assert make(hm, 60).kernel_name == 'hmpc::ric_kernel<3, 1, 60, 47>'   # compile-time N = 60
     assert make(hm, 10, 'f64_riccati').kernel_name == 'hmpc::ric_kernel<3, 2, 0, 0>'
-    assert make(hm, 20, 'f64_dense').kernel_name == 'hmpc::solve_kernel<3, 20, double>'
+    assert make(hm, 20, 'f64_dense').kernel_name == 'hmpc::solve_kernel<3, 20, double, 0, 0>'
     assert make(hm, 10, 'f64_generic').kernel_name == 'hmpc::wide_kernel<3, double>'
-    assert make(hm, 10, 'f32').kernel_name == 'hmpc::solve_kernel<3, 10, float>'
+    assert make(hm, 10, 'f32').kernel_name == 'hmpc::solve_kernel<3, 10, float, 0, 0>'
     assert make(hm, 20, 'f32').kernel_name == 'hmpc::wide_kernel<3, float>'   # no fp32 dense build
     assert make(hm, 10, 'f32_generic').kernel_name == 'hmpc::wide_kernel<3, float>'
 
 
 def test_active_capacity(hm):
-    # dense N = 10: QMAX = 20; Riccati: the largest R that keeps 8 (N <= 24)
+    # dense N = 10: the split's compacted kernel holds 13 (LDS for 3 waves /
+    # SIMD), the full one 20; Riccati: the largest R that keeps 8 (N <= 24)
     # or 4 workgroups per CU in LDS (hmpc_ric.hip ric_config)
-    assert make(hm, 10).active_capacity == 20
+    assert make(hm, 10).active_capacity == 13
     assert make(hm, 20).active_capacity == 38
     assert make(hm, 60).active_capacity == 47
     assert make(hm, 10, 'f64_riccati').active_capacity == 50

@@ -45,7 +45,7 @@ def test_fp32_dense_bounded(hm, variant, curve, musweep):
     inst = hmpc_plan.sample_instances(B, N, curve=curve, seed=91,
                                       mu_sweep=(0.3, 1.2) if musweep else None)
     g, name = solve(hm, 'f32', inst, N, variant)
-    assert name == f'hmpc::solve_kernel<{variant[0]}, 10, float>'
+    assert name == f'hmpc::solve_kernel<{variant[0]}, 10, float, 0, 0>'
     ref = port.solve_batch(variant, N, inst['x_in'], inst['x_lin'], inst['x_ref'], inst['pf'], inst['C'],
                            mu=inst['mu'], nthreads=16)
     assert np.array_equal(g['status'], ref['status'])

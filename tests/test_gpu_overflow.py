@@ -78,7 +78,7 @@ def solve_both(hm, N, inst, precision):
     return gpu, ref, kernel, cap
 
 
-@pytest.mark.parametrize('precision,kernel', [('f64', 'hmpc::solve_kernel<3, 10, double>'),
+@pytest.mark.parametrize('precision,kernel', [('f64', 'hmpc::solve_kernel<3, 10, double, 48, 13> + hmpc::solve_kernel<3, 10, double, 0, 0>'),
                                              ('f64_riccati', 'hmpc::ric_kernel<3, 2, 0, 0>')])
 def test_overflow_n10(hm, precision, kernel):
     N, B = 10, 48

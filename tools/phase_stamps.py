@@ -38,16 +38,30 @@ def main():
     st = out['x'].view(torch.int64).reshape(B, -1)[:, :len(NAMES) + 1].cpu().numpy()
     dur = np.diff(st, axis=1)
     tot = st[:, len(NAMES)] - st[:, 0]
-    res = {n: float(dur[:, i].mean()) for i, n in enumerate(NAMES)}
-    res['total_mean'] = float(tot.mean())
-    res['total_p50'] = float(np.median(tot))
-    res['total_max'] = float(tot.max())
-    res['iters_mean'] = float(out['iters'].float().mean())
-    # accumulated active-set sub-phases (slots 9..14 of the stamped build)
     acc = out['x'].view(torch.int64).reshape(B, -1)[:, 9:15].cpu().numpy()
-    for i, n in enumerate(['gi_scan', 'gi_fwd_sweep', 'gi_gram_schmidt', 'gi_bwd_sweep',
-                           'gi_dual_step', 'gi_add_drop']):
-        res[n] = float(acc[:, i].mean())
+    it = out['iters'].float().cpu().numpy()
+
+    def summary(m):
+        res = {n: float(dur[m, i].mean()) for i, n in enumerate(NAMES)}
+        res['total_mean'] = float(tot[m].mean())
+        res['total_p50'] = float(np.median(tot[m]))
+        res['total_max'] = float(tot[m].max())
+        res['iters_mean'] = float(it[m].mean())
+        res['instances'] = int(m.sum())
+        # accumulated active-set sub-phases (slots 9..14 of the stamped build)
+        for i, n in enumerate(['gi_scan', 'gi_fwd_sweep', 'gi_gram_schmidt', 'gi_bwd_sweep',
+                               'gi_dual_step', 'gi_add_drop']):
+            res[n] = float(acc[m, i].mean())
+        return res
+
+    # by class of the dense split launch: free variables nf = 3N + k * stance
+    nst = (inst['C'] != 0).sum(axis=1)
+    nf = 3 * N + (3 if var == '3f' else 2) * nst
+    cmp_nv = int(os.environ.get('CMP_NV', '48'))
+    res = {'all': summary(np.ones(B, bool)), 'compacted': summary(nf <= cmp_nv),
+           'full': summary(nf > cmp_nv)}
+    for s_ in np.unique(nst):
+        res[f'stance{int(s_)}_nf{int(3 * N + (3 if var == "3f" else 2) * s_)}'] = summary(nst == s_)
     print(json.dumps(res, indent=1))
 
 
