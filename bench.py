@@ -38,8 +38,18 @@ sys.path.insert(0, ROOT)
 
 METRIC = 'QP solves/sec (N=10, 3f) at batch=65k, 1→8 MI355X; max |u*−u*_cvxpy|'
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level table)
-FP64_VECTOR_PEAK_TFS = 78.6   # MI355X FP64 vector (half the 157.3 TF FP32 vector rate)
-FP32_VECTOR_PEAK_TFS = 157.3  # MI355X FP32 vector (MI355X_MICROARCH.md)
+FP64_VECTOR_SPEC_TFS = 78.6   # MI355X FP64 vector datasheet figure (half the FP32 vector rate)
+FP32_VECTOR_SPEC_TFS = 157.3  # MI355X FP32 vector (MI355X_MICROARCH.md)
+
+
+def measured_peaks():
+    """The vector FMA peaks measured on the box (tools/fp64_peak.hip, committed
+    as profiles/r03_fp64_peak.json); the datasheet figures when absent."""
+    p = os.path.join(ROOT, 'profiles', 'r03_fp64_peak.json')
+    if os.path.exists(p):
+        d = json.load(open(p))
+        return d['fp64_fma_tflops'], d['fp32_fma_tflops'], 'measured (profiles/r03_fp64_peak.json)'
+    return FP64_VECTOR_SPEC_TFS, FP32_VECTOR_SPEC_TFS, 'datasheet'
 
 
 def algorithmic_bytes(N, with_mu=True):
@@ -304,13 +314,23 @@ def main():
              f'{"" if args.precision == "f64" else "_" + args.precision}'
         tpath = os.path.join(ROOT, 'profiles', 'traffic.json')
         tj = json.load(open(tpath)).get(wl, {}) if os.path.exists(tpath) else {}
+        valu = None
         if tj.get('kernel') == kernel:
             traffic = tj.get('bytes_per_launch_x2_corrected')
             executed = None if 'float' in kernel else tj.get('fp64_flops_executed_per_solve')
+            if tj.get('valu_busy') is not None:
+                valu = {'busy': tj['valu_busy'], 'wait_any_frac': tj.get('wait_any_frac'),
+                        'valu_insts_per_solve': tj.get('valu_insts_per_solve'),
+                        'definition': 'SQ_ACTIVE_INST_VALU x 4 / (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs) '
+                                      'summed over the step\'s kernels: the fraction of SIMD cycles '
+                                      'issuing VALU work while they run',
+                        'source': tj.get('source')}
         total = B * world * args.steps
         f32 = 'float' in kernel
         vec_key = 'fp32_vector' if f32 else 'fp64_vector'
-        vec_peak = FP32_VECTOR_PEAK_TFS if f32 else FP64_VECTOR_PEAK_TFS
+        p64, p32, peak_src = measured_peaks()
+        vec_peak = p32 if f32 else p64
+        vec_spec = FP32_VECTOR_SPEC_TFS if f32 else FP64_VECTOR_SPEC_TFS
         rec = {
             'metric': METRIC,
             'value': total / el,
@@ -332,6 +352,12 @@ def main():
                        'precision': args.precision, 'parallelism': f'shard{world}'},
             'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS,
                          'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic,
+                         'limiter': 'not HBM: fp64 VALU issue (valu.busy) and dependent-chain latency of '
+                                    'an LDS/register-resident iterative solve (SURVEY 8d, DESIGN 5)',
+                         'hbm_note': 'the HBM roofline is unreachable by design: a solve moves '
+                                     f'{algorithmic_bytes(N)} B, so 40 % of 8 TB/s would need '
+                                     f'{0.4 * HBM_PEAK_GBS * 1e9 / algorithmic_bytes(N) / 1e6:.0f} M solves/s '
+                                     '(SURVEY 0.3 / 8d); the frac is reported, not targeted',
                          'traffic_over_algorithmic': traffic / (bpsolve * B) if traffic else None,
                          'kernel': kernel, 'kernel_ms': kern_ms, 'kernel_ms_max_rank': kern_ms_max,
                          'algorithmic_bytes_per_solve': bpsolve, 'solves_per_launch': B,
@@ -341,9 +367,12 @@ def main():
             # the bound that matters for this path: fp64 VALU
             vec_key: {
                 'achieved': flops * B / (kern_ms * 1e-3) / 1e12, 'peak': vec_peak,
+                'peak_source': peak_src, 'peak_spec': vec_spec,
                 'unit': 'TFLOP/s', 'frac': flops * B / (kern_ms * 1e-3) / 1e12 / vec_peak,
                 'flops_per_solve': flops, 'basis': 'algorithmic (bench.algorithmic_flops, DESIGN.md 5)',
-                'executed_flops_per_solve': executed},
+                'executed_flops_per_solve': executed,
+                'executed_frac': (executed * B / (kern_ms * 1e-3) / 1e12 / vec_peak) if executed else None},
+            'valu': valu,
             'cpu_baseline': base,
             'solved_frac_min_rank': float(sf[0]),
             'iters_mean': iters_mean, 'iters_max': int(it.max()),

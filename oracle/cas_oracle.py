@@ -26,7 +26,8 @@ The QP leaves x_N uncosted and only bounded above by its one-sided dynamics
 row, so the solution set is a ray in x_N.  u* and x_{<N} are unique (the
 rest of the Hessian is diagonal positive).  ``solve`` drops x_N and its
 rows, solves the rest exactly with ``qp_exact`` and reports x_N on its
-dynamics bound.  qpOASES's own answer is not reproducible here:
+dynamics bound (exact primal active-set method, oracle/qp_primal.py).
+qpOASES's own answer is not reproducible here:
 parity for this variant is unpinned against qpOASES; the problem data is
 pinned to the reference's own construction (tests/golden/cas_N10.npz,
 recorded through a casadi stub, tests/golden/_stubs/casadi).
@@ -35,7 +36,7 @@ from __future__ import annotations
 
 import numpy as np
 
-from oracle import qp_exact
+from oracle import qp_exact, qp_primal  # noqa: F401
 
 BIG = 1e10
 
@@ -137,7 +138,7 @@ def build_qp(t, N, m, g, mu, Jinv, rh, x_in, x_ref_in, C):
     ubx[nX + 2::n_u] = 400 * C
     lbx[nX + 2::n_u] = 0.0
     return dict(P=P, q=q, r=r, A=A, g0=np.array(g0), lbg=lbg, ubg=ubg, lbx=lbx, ubx=ubx,
-                Ad=Ad, Bd=Bd, Gd=Gd)
+                Ad=Ad, Bd=Bd, Gd=Gd, x_in=np.array(x_in, dtype=np.float64))
 
 
 def solve(qp, N):
@@ -164,7 +165,19 @@ def solve(qp, N):
     Ar, lo, hi = Ar[first], lo[first], hi[first]
     P = qp['P'][np.ix_(keep, keep)]
     q = qp['q'][keep]
-    res = qp_exact.solve(P, q, Ar, lo, hi)
+    # exact primal active-set solve (qp_primal) from a feasible point: zero
+    # inputs and the trajectory simulated through the dynamics rows meet every
+    # row (x_0 = x_in, each dynamics row at 0, forces 0 inside their bounds and
+    # friction cones).  qp_exact's IPM stalls on this degenerate QP (many
+    # one-sided dynamics rows active together) about once in six.
+    z0 = None
+    if 'Ad' in qp and 'x_in' in qp:
+        xs = np.zeros((N + 1, n_x))
+        xs[0] = qp['x_in']
+        for k in range(N):
+            xs[k + 1] = qp['Ad'] @ xs[k] + qp['Gd']
+        z0 = np.concatenate([xs.ravel(), np.zeros(n_u * N)])[keep]
+    res = qp_primal.solve(P, q, Ar, lo, hi, z0=z0)
     if res['x'] is None:
         return dict(z=None, u=None, x=None, status=res['status'], obj=np.nan)
     z = np.zeros(n)

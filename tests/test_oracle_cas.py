@@ -66,3 +66,42 @@ def test_reference_quirks_are_in_the_data(fx):
     fy1 = A[nd + 2 * N:nd + 3 * N + 1]
     np.testing.assert_array_equal(fy1[:N], fx1)
     assert (g['lbg'][0][:N + 1] == 0).all() and (g['lbg'][0][N + 1:] == -1e10).all()
+
+
+def test_primal_active_set_certifies_sampled_instances():
+    """oracle/qp_primal.py (exact primal active set from the simulated
+    zero-input trajectory) certifies every sampled CasADi QP -- the IPM of
+    qp_exact stalls on about one in six of these degenerate problems -- and
+    agrees with the IPM + polish wherever that one certifies."""
+    import warnings
+
+    import hmpc_plan
+    from oracle import cas_oracle as co
+    from oracle import qp_exact
+    N, B = 10, 16
+    inst = hmpc_plan.sample_instances(B, N, curve=True, seed=5)
+    c = hmpc_plan.runner_constants()
+    both = 0
+    for b in range(B):
+        qp = co.build_qp(0.02, N, c['m'], c['g'], 1.0, c['Jinv'], c['rh'], inst['x_in'][b], inst['x_ref'][b],
+                         inst['C'][b])
+        r = co.solve(qp, N)
+        assert r['status'] == 'solved', (b, r['status'])
+        z = r['z']
+        assert co.kkt_residual(qp, z, N) <= 1e-8
+        # the same reduced problem through the IPM route
+        keep = np.ones(len(z), bool)
+        keep[12 * N:12 * (N + 1)] = False
+        rows = ~np.any(qp['A'][:, ~keep] != 0.0, axis=1)
+        inf = lambda v: np.where(v >= co.BIG, np.inf, np.where(v <= -co.BIG, -np.inf, v))   # noqa: E731
+        Ar = np.vstack([qp['A'][rows][:, keep], np.eye(int(keep.sum()))])
+        lo = np.concatenate([inf(qp['lbg'][rows]) - qp['g0'][rows], inf(qp['lbx'][keep])])
+        hi = np.concatenate([inf(qp['ubg'][rows]) - qp['g0'][rows], inf(qp['ubx'][keep])])
+        fr = np.isinf(lo) & np.isinf(hi)
+        with warnings.catch_warnings():
+            warnings.simplefilter('ignore')
+            ipm = qp_exact.solve(qp['P'][np.ix_(keep, keep)], qp['q'][keep], Ar[~fr], lo[~fr], hi[~fr])
+        if ipm['status'] == 'solved':
+            both += 1
+            assert np.abs(ipm['x'] - z[keep]).max() <= 1e-7
+    assert both >= B // 2
