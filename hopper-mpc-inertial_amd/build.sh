@@ -29,7 +29,7 @@ cmp_flags() {
   done
 }
 for n in $HORIZONS; do
-  $HIPCC $FLAGS -DHMPC_INST_N=$n $(cmp_flags $n) -c csrc/hmpc_kernels.hip -o $BDIR/hmpc_kernels_n$n.o "$@" &
+  $HIPCC $FLAGS -DHMPC_INST_N=$n $(cmp_flags $n) -c ${KSRC:-csrc/hmpc_kernels.hip} -o $BDIR/hmpc_kernels_n$n.o "$@" &
   pids+=($!)
   while [ "$(jobs -rp | wc -l)" -ge "$JOBS" ]; do sleep 1; done
 done

@@ -8,6 +8,7 @@
 
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <string>
@@ -187,7 +188,11 @@ int prepare_ric(hmpc_ctx* c, int64_t B, hmpc::SolveArgs& a) {
   // the dense kernel's split launch (compacted kernel for the instances with
   // few free variables): class counts next to the overflow counters, which
   // the overflow pass zeroes together at its end
-  if (k == hmpc::Kernel::Dense && hmpc::dense_split_nv(c->N, false) > 0) {
+  // (HMPC_SPLIT=0 in the environment: one launch of the full kernel;
+  // HMPC_SPLIT_SERIAL=1: both classes on the caller's stream -- A/B switches)
+  static const bool split_off = getenv("HMPC_SPLIT") && getenv("HMPC_SPLIT")[0] == '0';
+  static const bool split_serial = getenv("HMPC_SPLIT_SERIAL") && getenv("HMPC_SPLIT_SERIAL")[0] == '1';
+  if (k == hmpc::Kernel::Dense && !split_off && hmpc::dense_split_nv(c->N, false) > 0) {
     if (B > c->split_cap) {
       if (c->split) (void)hipFree(c->split);
       c->split = nullptr;
@@ -206,9 +211,11 @@ int prepare_ric(hmpc_ctx* c, int64_t B, hmpc::SolveArgs& a) {
     }
     a.split_count = c->ovf + 3;
     a.split_list = c->split;
-    a.split_stream = c->split_stream;
-    a.split_fork = c->split_fork;
-    a.split_join = c->split_join;
+    if (!split_serial) {
+      a.split_stream = c->split_stream;
+      a.split_fork = c->split_fork;
+      a.split_join = c->split_join;
+    }
   }
   a.rws = c->rws;
   a.rws_stride = rstride;

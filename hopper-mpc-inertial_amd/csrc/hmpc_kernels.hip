@@ -512,13 +512,6 @@ __device__ __forceinline__ real tri_bwd(real acc, const real* Mc, const real* ze
 #define HMPC_TOC(slot, v) ((void)0)
 #endif
 
-// skip the Cholesky update FMAs of the padding columns (>= nf) chunk by
-// chunk (1), or update every column (0)
-#ifndef HMPC_CHUNK_SKIP
-#define HMPC_CHUNK_SKIP 0
-#endif
-constexpr bool kSkipChunks = HMPC_CHUNK_SKIP;
-
 // issue priority of the chain-bound phases: 0 off, 1 (default) the Cholesky
 // through the active set, 2 the Cholesky only.  A wave in its dependent
 // pivot/sweep chains issues first; the co-resident wave's throughput phases
@@ -1102,15 +1095,9 @@ solve_kernel(SolveArgs a) {
             }
           });
         };
-        // chunks holding columns < nf (uniform; k < nf so JA <= nf): the
-        // FMAs of the chunks beyond (padding columns) are skipped; their
-        // loads still issue, so every wait keeps its compile-time count
-        const int nchr = (nf - JA + CW - 1) / CW;
         load(std::integral_constant<int, 1>{});
         load(std::integral_constant<int, 2>{});
-        if constexpr (NCH > 0) {
-          if (!kSkipChunks || nchr > 0) update(std::integral_constant<int, 0>{}, nb);
-        }
+        if constexpr (NCH > 0) update(std::integral_constant<int, 0>{}, nb);
         if constexpr (k + 1 < NV) ahead(std::integral_constant<int, k + 1>{});
         sfor<1, NCH>([&](auto chc) __attribute__((always_inline)) {
           constexpr int ch = decltype(chc)::value;
@@ -1121,10 +1108,15 @@ solve_kernel(SolveArgs a) {
                                 : ch == 2 ? NAHEAD + nl(JA, 3) + nl(JA, 4)
                                           : nl(JA, ch + 1) + nl(JA, ch + 2);
           lds_wait<younger>(buf[ch % 3][0], buf[ch % 3][1]);
-          if (!kSkipChunks || ch < nchr) update(chc, buf[ch % 3]);
+          update(chc, buf[ch % 3]);
         });
       });
-      // the last step's lookahead loaded a padding column: drain it
+      // the last step's lookahead loaded a padding column: drain it.  (The
+      // ladder's exits merge here with that load in flight; the register
+      // allocation is checked to keep nb in place -- tools/feas_diag.py on
+      // the GPU; a front-padded variant whose per-step branches made the
+      // compiler copy in-flight lookahead registers returned wrong optima,
+      // DESIGN.md 7)
       lds_wait<0>(nb[0], nb[1]);
     } else {
       real mine = Rg[0];   // A[tid][k] of the current step
