@@ -517,8 +517,17 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
   // DPP inside asm, so the block covers the worst hazard in front of it
   // itself -- an SALU write of EXEC (the lane < 6 stores) followed by a DPP
   // op needs 5 wait states (a VALU write of x, 2).
-#define HMPC_DPPF(acc, x, k, n) "v_fmac_f64_dpp %" #acc ", %" #x ", %" #k " row_newbcast:" #n " row_mask:0xf bank_mask:0xf\n\t"
-#define HMPC_DPPFN(acc, x, k, n) "v_fmac_f64_dpp %" #acc ", %" #x ", -%" #k " row_newbcast:" #n " row_mask:0xf bank_mask:0xf\n\t"
+#ifndef HMPC_OVF_DPP
+#define HMPC_OVF_DPP 0   // 1: the DPP blocks in the overflow pass too (A/B)
+#endif
+#ifndef HMPC_DPP_TAIL
+#define HMPC_DPP_TAIL ""   // A/B: "s_nop 4" after every block
+#endif
+#ifndef HMPC_DPP_BC
+#define HMPC_DPP_BC ""     // A/B: " bound_ctrl:1" (a disabled source lane reads 0)
+#endif
+#define HMPC_DPPF(acc, x, k, n) "v_fmac_f64_dpp %" #acc ", %" #x ", %" #k " row_newbcast:" #n " row_mask:0xf bank_mask:0xf" HMPC_DPP_BC "\n\t"
+#define HMPC_DPPFN(acc, x, k, n) "v_fmac_f64_dpp %" #acc ", %" #x ", -%" #k " row_newbcast:" #n " row_mask:0xf bank_mask:0xf" HMPC_DPP_BC "\n\t"
   struct BwdL {
     double cp, sp, st, b0, b1, b2, n, kc[6];
   };
@@ -599,10 +608,10 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
         }
         // B_j'lam over lam[6..11] (lanes 6..11 of li)
         double bc;
-        if constexpr (ENT == 1) {
+        if constexpr (ENT == 1 || HMPC_OVF_DPP) {
           double bc0 = 0.0, bc1 = 0.0;
           asm("s_nop 4\n\t" HMPC_DPPF(0, 2, 3, 6) HMPC_DPPF(1, 2, 4, 7) HMPC_DPPF(0, 2, 5, 8)
-              HMPC_DPPF(1, 2, 6, 9) HMPC_DPPF(0, 2, 7, 10) HMPC_DPPF(1, 2, 8, 11)
+              HMPC_DPPF(1, 2, 6, 9) HMPC_DPPF(0, 2, 7, 10) HMPC_DPPF(1, 2, 8, 11) HMPC_DPP_TAIL
               : "+v"(bc0), "+v"(bc1)
               : "v"(li), "v"(k6), "v"(k7), "v"(k8), "v"(d.b0), "v"(d.b1), "v"(d.b2));
           bc = bc0 + bc1;
@@ -619,9 +628,9 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
         const double s6 = row_shift<-6>(li), s5 = row_shift<-5>(li), s7 = row_shift<-7>(li);
         double a0 = fma(fma(gB, d.cp, gA), s6, li), a1 = (gC * d.sp) * s5, a2 = (gD * d.sp) * s7;
         // + K_j[:, i]'mu_j, mu_j in lanes 0..5 of m
-        if constexpr (ENT == 1) {
+        if constexpr (ENT == 1 || HMPC_OVF_DPP) {
           asm("s_nop 4\n\t" HMPC_DPPF(0, 3, 4, 0) HMPC_DPPF(1, 3, 5, 1) HMPC_DPPF(2, 3, 6, 2)
-              HMPC_DPPF(0, 3, 7, 3) HMPC_DPPF(1, 3, 8, 4) HMPC_DPPF(2, 3, 9, 5)
+              HMPC_DPPF(0, 3, 7, 3) HMPC_DPPF(1, 3, 8, 4) HMPC_DPPF(2, 3, 9, 5) HMPC_DPP_TAIL
               : "+v"(a0), "+v"(a1), "+v"(a2)
               : "v"(m), "v"(d.kc[0]), "v"(d.kc[1]), "v"(d.kc[2]), "v"(d.kc[3]), "v"(d.kc[4]), "v"(d.kc[5]));
         } else {
@@ -696,11 +705,11 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
       auto fstep = [&](int k, const FwdL& d) __attribute__((always_inline)) {
         // u = w - K_k x (x in lanes 0..11 of xi)
         double a0 = d.w, a1 = 0.0;
-        if constexpr (ENT == 1) {
+        if constexpr (ENT == 1 || HMPC_OVF_DPP) {
           asm("s_nop 4\n\t" HMPC_DPPFN(0, 2, 3, 0) HMPC_DPPFN(1, 2, 4, 1) HMPC_DPPFN(0, 2, 5, 2)
               HMPC_DPPFN(1, 2, 6, 3) HMPC_DPPFN(0, 2, 7, 4) HMPC_DPPFN(1, 2, 8, 5)
               HMPC_DPPFN(0, 2, 9, 6) HMPC_DPPFN(1, 2, 10, 7) HMPC_DPPFN(0, 2, 11, 8)
-              HMPC_DPPFN(1, 2, 12, 9) HMPC_DPPFN(0, 2, 13, 10) HMPC_DPPFN(1, 2, 14, 11)
+              HMPC_DPPFN(1, 2, 12, 9) HMPC_DPPFN(0, 2, 13, 10) HMPC_DPPFN(1, 2, 14, 11) HMPC_DPP_TAIL
               : "+v"(a0), "+v"(a1)
               : "v"(xi), "v"(d.kr[0]), "v"(d.kr[1]), "v"(d.kr[2]), "v"(d.kr[3]), "v"(d.kr[4]), "v"(d.kr[5]),
                 "v"(d.kr[6]), "v"(d.kr[7]), "v"(d.kr[8]), "v"(d.kr[9]), "v"(d.kr[10]), "v"(d.kr[11]));
@@ -731,9 +740,9 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
         const double r3 = m911 * d.br[3], r4 = m911 * d.br[4], r5 = m911 * d.br[5];
         double b0 = fma(fma(fB, d.cp, fA), s6, xi), b1 = (fC * d.sp) * s7, b2 = (fD * d.sp) * s5;
         // + B_k u_k, u_k in lanes 0..5 of u
-        if constexpr (ENT == 1) {
+        if constexpr (ENT == 1 || HMPC_OVF_DPP) {
           asm("s_nop 4\n\t" HMPC_DPPF(0, 3, 4, 0) HMPC_DPPF(1, 3, 5, 1) HMPC_DPPF(2, 3, 6, 2)
-              HMPC_DPPF(0, 3, 7, 3) HMPC_DPPF(1, 3, 8, 4) HMPC_DPPF(2, 3, 9, 5)
+              HMPC_DPPF(0, 3, 7, 3) HMPC_DPPF(1, 3, 8, 4) HMPC_DPPF(2, 3, 9, 5) HMPC_DPP_TAIL
               : "+v"(b0), "+v"(b1), "+v"(b2)
               : "v"(u), "v"(r0), "v"(r1), "v"(r2), "v"(r3), "v"(r4), "v"(r5));
         } else {
