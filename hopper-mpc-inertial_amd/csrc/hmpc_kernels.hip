@@ -1509,6 +1509,31 @@ solve_kernel(SolveArgs a) {
       }
     }
   }
+#if defined(HMPC_REFINE_LB) && HMPC_REFINE_LB > 0
+  // A/B lower bound of fp32 + iterative refinement (configs[4]):
+  // HMPC_REFINE_LB range-space corrections on the final active set -- a
+  // forward sweep, Gram-Schmidt against Qw, a backward sweep each -- scaled by
+  // a run-time zero.  The solve cost a refinement adds before its fp64
+  // residuals (not included); results unchanged.
+  if constexpr (kF32) {
+    const real z0 = sm[L::ZR];
+    real acc = v;
+    const int qu = uni(q);
+#pragma unroll 1
+    for (int it = 0; it < HMPC_REFINE_LB; ++it) {
+      real wp = tri_fwd_lds<L>(acc, Lc, zero, dinv, xs, nf, 0);
+      ladder<0, QMAX>(qu, [&](auto lc) __attribute__((always_inline)) {
+        constexpr int l = decltype(lc)::value;
+        const real cl = B::sum(Qw[l] * wp, red);
+        wp = fma(-cl, Qw[l], wp);
+      });
+      B::sync();
+      const real zi = tri_bwd<L>(wp, Lc, zero, dinv, xs, nf);
+      acc = fma(z0, zi, acc);
+    }
+    v = acc;
+  }
+#endif
   HMPC_STAMP(7);
   if constexpr (HMPC_PRIO != 0) __builtin_amdgcn_s_setprio(0);
 

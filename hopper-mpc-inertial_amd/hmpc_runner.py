@@ -14,7 +14,8 @@ The plan (``path_plan_init``, one per robot from its own start state, or one
 shared plan when all robots start alike) and the gait schedule (``gait_map``
 per MPC call, ``gait_scheduler`` per step) are made on the device too
 (``hmpc_plan_batch`` / ``hmpc_gait_batch``), so a period is two kernel
-launches and no host work.
+launches and no host work; ``run(graph=True)`` replays the whole run as
+one captured HIP graph.
 Plots are out of scope.
 
 There is no CPU fallback: without libhmpc.so or a GPU this raises.
@@ -52,24 +53,73 @@ class Runner:
         self.X0 = np.ascontiguousarray(np.broadcast_to(X0, (self.B, 13)))
         # X_f = [dist, 0, 0.27, 1, 0 ...] (:58)
         self.X_f = np.hstack([self.cfg.dist, 0, 0.27, 1, np.zeros(9)]).astype(np.float64)
+        self._graphs = {}     # (steps, record) -> (graph, buffers, stream)
+        self._x0_ver = 0
 
     def close(self):
         self.ctx.close()
 
-    def run(self, n_periods=None, record=True):
+    def run(self, n_periods=None, record=True, graph=False):
         """Runner.run (src/robotrunner.py:81-113) without plots.
 
         Runs the first ``n_periods`` MPC periods (all of N_run when None).
         Returns numpy arrays X_traj (B, steps+1, 13), f_hist (B, steps, 6),
-        s_hist (steps,), plus per-call status (n_calls, B) and the plan."""
+        s_hist (steps,), plus per-call status (n_calls, B) and the plan.
+
+        ``graph=True``: the periods (every mpcontrol, plant step and record
+        copy: 5-8 launches per period) are captured once into a HIP graph on
+        the Runner's own stream and replayed by later ``graph=True`` runs of
+        the same length -- one graph launch per run instead of one host
+        launch per kernel.  The first such call runs eagerly (it allocates
+        the context's workspaces, which a capture cannot) and captures; a
+        replay first re-plans on the device when the start states changed
+        (``set_start``).  Results equal the eager run's bit for bit."""
+        import torch
+        steps = self._steps(n_periods)
+        if not graph:
+            S = self._setup(steps, record)
+            self._enqueue(S)
+            return self._finish(S)
+        key = (steps, bool(record))
+        g = self._graphs.get(key)
+        if g is None:
+            stream = torch.cuda.Stream(self.device)
+            stream.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(stream):
+                S = self._setup(steps, record)
+                self._enqueue(S)          # eager: workspaces allocated, results valid
+            stream.synchronize()
+            res = self._finish(S)
+            cg = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(cg, stream=stream):
+                self._enqueue(S)
+            self._graphs[key] = (cg, S, stream)
+            return res
+        cg, S, stream = g
+        with torch.cuda.stream(stream):
+            if S['x0_ver'] != self._x0_ver:
+                self._replan(S)
+            cg.replay()
+        stream.synchronize()
+        return self._finish(S)
+
+    def set_start(self, X0):
+        """New start states X_0 (13,) or (B, 13) for the next run (graph
+        replays re-plan from them on the device)."""
+        X0 = np.asarray(X0, dtype=np.float64)
+        self.X0 = np.ascontiguousarray(np.broadcast_to(X0, (self.B, 13)))
+        self._x0_ver += 1
+
+    def _steps(self, n_periods):
+        cfg = self.cfg
+        return cfg.N_run if n_periods is None else min(cfg.N_run, int(n_periods) * cfg.mpc_factor)
+
+    def _plan(self, X0buf, x_in):
+        """convert(X_0) and path_plan_init on the device (:91,102)."""
         import torch
         cfg, B, dev = self.cfg, self.B, self.device
-        N, mf, dt = cfg.N, cfg.mpc_factor, cfg.dt
-        steps = cfg.N_run if n_periods is None else min(cfg.N_run, int(n_periods) * mf)
         f64 = dict(dtype=torch.float64, device=dev)
-        X = torch.from_numpy(self.X0.copy()).to(dev)
-        x_in = torch.empty((B, 12), **f64)
-        self.ctx.convert_device(X, x_in)                                         # :102
+        self.ctx.convert_device(X0buf, x_in)                                      # :102
         # plan on the device: path_plan_init(convert(X_0), convert(X_f)) (:91),
         # one plan per robot -- or one shared plan when every robot starts alike
         shared = bool((self.X0 == self.X0[:1]).all())
@@ -78,47 +128,98 @@ class Runner:
         xf = torch.empty((Bp, 12), **f64)
         self.ctx.convert_device(Xf, xf)
         x0p = x_in[:1].clone() if shared else x_in.clone()
-        plan_x, plan_pf, _ = self.ctx.plan_device(x0p, xf, cfg.N_run, cfg.N_k, dt, cfg.curve, cfg.t_p,
+        plan_x, plan_pf, _ = self.ctx.plan_device(x0p, xf, cfg.N_run, cfg.N_k, cfg.dt, cfg.curve, cfg.t_p,
                                                   cfg.phi_switch, cfg.t_start, cfg.step_adjustment)
-        T = plan_x.shape[1]
         if shared:
             plan_x, plan_pf = plan_x[0], plan_pf[0]
+        return shared, plan_x, plan_pf
+
+    def _setup(self, steps, record):
+        """Device buffers, plan and gait schedule of one run."""
+        import torch
+        cfg, B, dev = self.cfg, self.B, self.device
+        N, mf, dt = cfg.N, cfg.mpc_factor, cfg.dt
+        f64 = dict(dtype=torch.float64, device=dev)
+        X0buf = torch.from_numpy(self.X0.copy()).to(dev)
+        x_in = torch.empty((B, 12), **f64)
+        shared, plan_x, plan_pf = self._plan(X0buf, x_in)
         # gait schedule per low-level step and per MPC call, on the device
         # (the reference's float64 time accumulation, :92-101)
         C_all, s_hist_d = self.ctx.gait_device(steps, mf, N, dt, cfg.mpc_dt, cfg.t_p, cfg.phi_switch,
                                                cfg.t_start, 0.0)
         call_k = list(range(0, steps, mf))
+        S = dict(steps=steps, record=record, X0buf=X0buf, x_in=x_in, shared=shared, plan_x=plan_x,
+                 plan_pf=plan_pf, C_all=C_all, s_hist=s_hist_d, call_k=call_k,
+                 x0_ver=self._x0_ver,
+                 X=torch.empty((B, 13), **f64),
+                 x_prev=torch.zeros((B, N + 1, 12), **f64),
+                 out=dict(u=torch.empty((B, N, 6), **f64), obj=torch.empty(B, **f64),
+                          status=torch.empty(B, dtype=torch.int32, device=dev),
+                          iters=torch.empty(B, dtype=torch.int32, device=dev)),
+                 X_traj=torch.empty((B, steps + 1, 13), **f64) if record else None,
+                 f_hist=torch.empty((B, steps, 6), **f64) if record else None,
+                 hist=torch.empty((B, mf, 13), **f64) if record else None,
+                 status=torch.empty((len(call_k), B), dtype=torch.int32, device=dev))
+        return S
+
+    def _replan(self, S):
+        """A replay with new start states: the plan again, into the captured
+        buffers (the planner's error check syncs, so it stays out of the graph)."""
+        S['X0buf'].copy_(torch_from(self.X0, S['X0buf']))
+        shared, plan_x, plan_pf = self._plan(S['X0buf'], S['x_in'])
+        if shared != S['shared']:
+            raise ValueError('a graph replay cannot switch between a shared and per-robot plans; '
+                             'run with graph=False or use a new Runner')
+        S['plan_x'].copy_(plan_x)
+        S['plan_pf'].copy_(plan_pf)
+        S['x0_ver'] = self._x0_ver
+
+    def _enqueue(self, S):
+        """The MPC periods (:92-113) on the current stream, no host work: what
+        a graph captures."""
+        cfg, B = self.cfg, self.B
+        N, mf, dt = cfg.N, cfg.mpc_factor, cfg.dt
+        steps, record = S['steps'], S['record']
+        X, x_in, x_prev, out = S['X'], S['x_in'], S['x_prev'], S['out']
+        X.copy_(S['X0buf'])
+        self.ctx.convert_device(X, x_in)                                         # :102
+        x_prev.zero_()
+        plan_x, plan_pf = S['plan_x'], S['plan_pf']
+        T = plan_x.shape[-2]
         pf_flat = plan_pf.reshape(-1)
-        pf_bs = 0 if shared else 3 * T
-        x_prev = torch.zeros((B, N + 1, 12), **f64)
-        out = dict(u=torch.empty((B, N, 6), **f64), obj=torch.empty(B, **f64),
-                   status=torch.empty(B, dtype=torch.int32, device=dev),
-                   iters=torch.empty(B, dtype=torch.int32, device=dev))
-        X_traj = torch.empty((B, steps + 1, 13), **f64) if record else None
-        f_hist = torch.empty((B, steps, 6), **f64) if record else None
-        hist = torch.empty((B, mf, 13), **f64) if record else None
+        pf_bs = 0 if S['shared'] else 3 * T
+        X_traj, f_hist, hist = S['X_traj'], S['f_hist'], S['hist']
         if record:
             X_traj[:, 0] = X
-        status = torch.empty((len(call_k), B), dtype=torch.int32, device=dev)
-        for p, k in enumerate(call_k):
-            self.ctx.mpcontrol_plan_device(p == 0, x_in, plan_x, plan_pf, k, mf, C_all[p], x_prev,
+        for p, k in enumerate(S['call_k']):
+            self.ctx.mpcontrol_plan_device(p == 0, x_in, plan_x, plan_pf, k, mf, S['C_all'][p], x_prev,
                                            out=out)                             # :98-103
-            status[p] = out['status']
+            S['status'][p] = out['status']
             n = min(mf, steps - k)
             self.ctx.plant_device(X, out['u'], 6 * N, pf_flat[3 * k:], pf_bs, 3, n, dt, self.J,
                                   X_hist=hist if record else None, x_out=x_in)   # :109-111
             if record:
                 X_traj[:, k + 1:k + 1 + n] = hist[:, :n]
                 f_hist[:, k:k + n] = out['u'][:, 0:1, :]
-        torch.cuda.synchronize(dev)
-        st = status.cpu().numpy()
+
+    def _finish(self, S):
+        import torch
+        torch.cuda.synchronize(self.device)
+        st = S['status'].cpu().numpy()
         if (st != 0).any():
             bad = np.argwhere(st != 0)[0]
             raise Exception(f"\n *** QP FAILED *** \n (call {bad[0]}, robot {bad[1]}: "
                             f"{hmpc.STATUS.get(int(st[bad[0], bad[1]]), st[bad[0], bad[1]])})")
-        res = dict(X_final=X.cpu().numpy(), s_hist=s_hist_d.cpu().numpy(), status=st,
-                   x_ref=plan_x.cpu().numpy(), pf_ref=plan_pf.cpu().numpy(), call_k=np.array(call_k))
-        if record:
-            res['X_traj'] = X_traj.cpu().numpy()
-            res['f_hist'] = f_hist.cpu().numpy()
+        res = dict(X_final=S['X'].cpu().numpy(), s_hist=S['s_hist'].cpu().numpy(), status=st,
+                   x_ref=S['plan_x'].cpu().numpy(), pf_ref=S['plan_pf'].cpu().numpy(),
+                   call_k=np.array(S['call_k']))
+        if S['record']:
+            res['X_traj'] = S['X_traj'].cpu().numpy()
+            res['f_hist'] = S['f_hist'].cpu().numpy()
         return res
+
+
+def torch_from(a, like):
+    """numpy array -> tensor on `like`'s device."""
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(a)).to(like.device)

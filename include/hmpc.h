@@ -219,8 +219,10 @@ int hmpc_gait_batch(hmpc_ctx* ctx, int n_steps, int mpc_factor, int N, double dt
 int hmpc_set_precision(hmpc_ctx* ctx, int precision);
 
 /* Name of the solve kernel this context's (variant, N, precision) runs on,
-   e.g. "hmpc::solve_kernel<3, 10, double>" or "hmpc::ric_kernel<3, 2, 0, 0>" (static string;
-   "" when none).  For benchmark records and profiles. */
+   as rocprofv3 demangles it, e.g. "hmpc::ric_kernel<3, 2, 0, 0>"; a split launch names
+   both kernels, "hmpc::solve_kernel<3, 10, double, 48, 13> + hmpc::solve_kernel<3, 10,
+   double, 0, 0>" (the compacted one first).  Static string, "" when none.  For benchmark
+   records and profiles. */
 const char* hmpc_kernel_name(hmpc_ctx* ctx);
 
 /* Active-set capacity of that kernel's main pass (-1 when none): instances

@@ -188,3 +188,30 @@ def test_run_cli_mirror(hm, tmp_path):
     d = np.load(out)
     assert d['X_traj'].shape == (2, 201, 13) and (res['status'] == 0).all()
     np.testing.assert_array_equal(d['X_traj'][0], d['X_traj'][1])   # same start state
+
+
+def test_runner_graph_replay_equals_eager(hm):
+    """run(graph=True): the first call runs eagerly and captures the periods
+    into a HIP graph, later calls replay it (re-planning on the device after
+    set_start).  Every replay equals the eager run bit for bit."""
+    import hmpc_runner
+    B, n = 4, 12
+    rng = np.random.default_rng(5)
+    X0 = np.tile(hmpc_runner.X0_DEFAULT, (B, 1))
+    X0[:, 0:3] += rng.uniform(-0.01, 0.01, (B, 3))
+    X0b = X0.copy()
+    X0b[:, 7:10] += rng.uniform(-0.05, 0.05, (B, 3))
+    r = hmpc_runner.Runner(dyn='3f', curve=True, N_run=400, N=10, batch=B, X0=X0)
+    e = r.run(n_periods=n)
+    g1 = r.run(n_periods=n, graph=True)
+    g2 = r.run(n_periods=n, graph=True)
+    r.set_start(X0b)
+    g3 = r.run(n_periods=n, graph=True)
+    r.close()
+    rb = hmpc_runner.Runner(dyn='3f', curve=True, N_run=400, N=10, batch=B, X0=X0b)
+    eb = rb.run(n_periods=n)
+    rb.close()
+    for got, want in ((g1, e), (g2, e), (g3, eb)):
+        for k in ('X_traj', 'f_hist', 'status', 'x_ref', 'pf_ref'):
+            np.testing.assert_array_equal(got[k], want[k], err_msg=k)
+    assert not np.array_equal(e['X_traj'], eb['X_traj'])

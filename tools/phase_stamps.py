@@ -27,7 +27,8 @@ def main():
     N = int(os.environ.get('N', '10'))
     B = int(os.environ.get('B', '65536'))
     var = os.environ.get('VARIANT', '3f')
-    inst = hmpc_plan.sample_instances(B, N, curve=True, seed=2024)
+    curve = os.environ.get('STRAIGHT', '0') != '1'
+    inst = hmpc_plan.sample_instances(B, N, curve=curve, seed=2024)
     d = {k: torch.from_numpy(np.ascontiguousarray(inst[k])).cuda()
          for k in ('x_in', 'x_lin', 'x_ref', 'pf', 'C', 'mu')}
     c = ho.runner_constants()
@@ -62,6 +63,16 @@ def main():
            'full': summary(nf > cmp_nv)}
     for s_ in np.unique(nst):
         res[f'stance{int(s_)}_nf{int(3 * N + (3 if var == "3f" else 2) * s_)}'] = summary(nst == s_)
+    # timeline of the launch (raw s_memtime; one clock domain per XCD, so
+    # quantiles over the batch, not exact offsets): when instances start and
+    # end relative to the first start -- dispatch delay vs instance latency
+    t0 = st[:, 0] - st[:, 0].min()
+    t1 = st[:, len(NAMES)] - st[:, 0].min()
+    q = [0.0, 0.5, 0.9, 0.99, 1.0]
+    res['timeline'] = {'start_quantiles': [float(np.quantile(t0, x)) for x in q],
+                       'end_quantiles': [float(np.quantile(t1, x)) for x in q],
+                       'latency_quantiles': [float(np.quantile(tot, x)) for x in q],
+                       'quantiles': q}
     print(json.dumps(res, indent=1))
 
 

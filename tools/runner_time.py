@@ -1,7 +1,8 @@
 """Wall time of the device Runner (hmpc_runner.Runner.run: plan + gait +
 100 MPC periods of mpcontrol_plan + plant) for the reference's configs[0]
 (run.py 3f --N_run=2000, N = 60) at batch 1 and a few batch sizes.
-python tools/runner_time.py [graph]"""
+python tools/runner_time.py [graph]     (graph: timed run = a replay of the
+captured run, hmpc_runner.Runner.run(graph=True))"""
 import json
 import os
 import sys
@@ -21,7 +22,8 @@ for B in (1, 256, 4096):
     kw = dict(record=False)
     if graph:
         kw['graph'] = True
-    r.run(n_periods=2, **kw)          # warm (workspaces, code objects)
+    # warm (workspaces, code objects); graph: the full-length run captures
+    r.run(n_periods=None if graph else 2, **kw)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     out = r.run(**kw)
