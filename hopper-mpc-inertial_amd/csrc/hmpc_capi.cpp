@@ -394,7 +394,10 @@ const char* hmpc_kernel_name(hmpc_ctx* c) {
     case hmpc::Kernel::Riccati:
       // (template arguments as rocprofv3 demangles them: variant, occupancy,
       // compile-time horizon and capacity, 0 = runtime)
-      if (hmpc::ric_occ(c->N) == 2) return v3 ? "hmpc::ric_kernel<3, 2, 0, 0>" : "hmpc::ric_kernel<2, 2, 0, 0>";
+      if (hmpc::ric_occ(c->N) == 2) {
+        if (hmpc::ric_static_n(c->N) == 20) return v3 ? "hmpc::ric_kernel<3, 2, 20, 38>" : "hmpc::ric_kernel<2, 2, 20, 38>";
+        return v3 ? "hmpc::ric_kernel<3, 2, 0, 0>" : "hmpc::ric_kernel<2, 2, 0, 0>";
+      }
       if (hmpc::ric_static_n(c->N) == 60) return v3 ? "hmpc::ric_kernel<3, 1, 60, 47>" : "hmpc::ric_kernel<2, 1, 60, 47>";
       return v3 ? "hmpc::ric_kernel<3, 1, 0, 0>" : "hmpc::ric_kernel<2, 1, 0, 0>";
     case hmpc::Kernel::Wide:

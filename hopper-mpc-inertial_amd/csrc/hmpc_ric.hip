@@ -1289,7 +1289,9 @@ int ric_qcap(int N) { return ric_config(N).cap; }
 int ric_occ(int N) { return ric_config(N).occ; }
 int ric_static_n(int N) {
   const RicCfg c = ric_config(N);
-  return (N == 60 && c.occ == 1 && c.cap == 47) ? 60 : 0;
+  if (N == 60 && c.occ == 1 && c.cap == 47) return 60;
+  if (N == 20 && c.occ == 2 && c.cap == 38) return 20;
+  return 0;
 }
 
 // K / Dinv of every stage, then the cached columns H^-1 n_a (capacity x NV)
@@ -1312,15 +1314,18 @@ bool ric_launch_k(K kern, int N, int cap, const SolveArgs& a, hipStream_t s, int
   hipLaunchKernelGGL(kern, dim3(g), dim3(RT), lds, s, a, N, cap);
   return true;
 }
-// the Runner's horizon N = 60 has a compile-time instantiation, used when the
-// host-side configuration matches the one it was built for: +7 % at B = 4096.
-// (N = 20 at 2 waves/SIMD measured 6 % slower that way: it spills at the
-// 256-VGPR cap, so configs[3] keeps the runtime-N kernel.)
+// the Runner's horizon N = 60 and configs[3]'s N = 20 have compile-time
+// instantiations, used when the host-side configuration matches the one they
+// were built for: +7 % at N = 60 (B = 4096), +1.4 % at N = 20 (B = 262144;
+// 12 B/lane of scratch at the 2-wave 256-VGPR cap since the round-2 register
+// savings -- it lost 6 % when it spilled more)
 template <int VAR, int OCC>
 bool ric_launch(int N, const SolveArgs& a, hipStream_t s, int* per) {
   const int cap = ric_qcap(N);
   if constexpr (OCC == 1) {
     if (ric_static_n(N) == 60) return ric_launch_k(ric_kernel<VAR, OCC, 60, 47>, N, cap, a, s, per);
+  } else {
+    if (ric_static_n(N) == 20) return ric_launch_k(ric_kernel<VAR, OCC, 20, 38>, N, cap, a, s, per);
   }
   return ric_launch_k(ric_kernel<VAR, OCC>, N, cap, a, s, per);
 }

@@ -36,7 +36,7 @@ def _free_port():
 
 # name -> (horizon, --curve, global batch or 0 = PER_RANK per rank, kernel)
 WORKLOADS = {'cfg2_weak': (N, True, 0, 'hmpc::solve_kernel<3, 10, double, 48, 13> + hmpc::solve_kernel<3, 10, double, 0, 0>'),
-             'cfg3_strong': (20, False, 4097, 'hmpc::ric_kernel<3, 2, 0, 0>')}
+             'cfg3_strong': (20, False, 4097, 'hmpc::ric_kernel<3, 2, 20, 38>')}
 
 
 def _ctx(hmpc, n=N):

@@ -27,8 +27,8 @@ def hm():
 
 @pytest.mark.parametrize('variant,N,B,curve,kernel', [
     ('3f', 13, 2048, True, 'hmpc::ric_kernel<3, 2, 0, 0>'),
-    ('3f', 20, 4096, False, 'hmpc::ric_kernel<3, 2, 0, 0>'),
-    ('2f', 20, 2048, True, 'hmpc::ric_kernel<2, 2, 0, 0>'),
+    ('3f', 20, 4096, False, 'hmpc::ric_kernel<3, 2, 20, 38>'),
+    ('2f', 20, 2048, True, 'hmpc::ric_kernel<2, 2, 20, 38>'),
     ('3f', 40, 1024, True, 'hmpc::ric_kernel<3, 1, 0, 0>'),
     ('3f', 60, 1024, False, 'hmpc::ric_kernel<3, 1, 60, 47>'),
 ])
