@@ -645,7 +645,24 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
       };
       // (loads are unconditional -- out-of-range steps reload stage 0 -- so
       // that the vmcnt/lgkmcnt waits stay counted, not drained)
-      if constexpr (RING == 3) {
+      if constexpr (RING >= 4) {   // RING-deep (1 wave/SIMD: K loads that miss L2)
+        BwdL R[RING];
+#pragma unroll
+        for (int p = 0; p < RING - 1; ++p) load_b(jt >= p ? jt - p : 0, R[p]);
+        for (int j = jt; j >= 0; j -= RING) {
+          bool go = true;
+#pragma unroll
+          for (int i = 0; i < RING; ++i) {
+            if (go) {
+              const int jj = j - i, jl = jj - (RING - 1);
+              load_b(jl >= 0 ? jl : 0, R[(i + RING - 1) % RING]);
+              bstep(jj, R[i]);
+              if (jj < 1) go = false;
+            }
+          }
+          if (!go) break;
+        }
+      } else if constexpr (RING == 3) {
         BwdL R0, R1, R2;
         load_b(jt, R0);
         load_b(jt >= 1 ? jt - 1 : 0, R1);
@@ -755,7 +772,24 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
         }
         xi = lane < 12 ? (b0 + b1) + b2 : 0.0;
       };
-      if constexpr (RING == 3) {
+      if constexpr (RING >= 4) {
+        FwdL R[RING];
+#pragma unroll
+        for (int p = 0; p < RING - 1; ++p) load_f(p < N ? p : N - 1, R[p]);
+        for (int k = 0; k < N; k += RING) {
+          bool go = true;
+#pragma unroll
+          for (int i = 0; i < RING; ++i) {
+            if (go) {
+              const int kk = k + i, kl = kk + RING - 1;
+              load_f(kl < N ? kl : N - 1, R[(i + RING - 1) % RING]);
+              fstep(kk, R[i]);
+              if (kk + 1 >= N) go = false;
+            }
+          }
+          if (!go) break;
+        }
+      } else if constexpr (RING == 3) {
         FwdL R0, R1, R2;
         load_f(0, R0);
         load_f(N >= 2 ? 1 : 0, R1);
@@ -1208,6 +1242,11 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
 // overflow count before the launch) until the batch is done.
 // OCC = waves per SIMD the register allocation is held to (2: <= 256 VGPRs +
 // AGPRs; 1: up to 512)
+// sweep prefetch depth (ring slots) at 1 wave/SIMD
+#ifndef HMPC_RIC_RING1
+#define HMPC_RIC_RING1 3
+#endif
+constexpr int kRing1Wave = HMPC_RIC_RING1;
 template <int VAR, int OCC, int NC = 0, int CAPC = 0>
 __global__ void __launch_bounds__(RT) __attribute__((amdgpu_waves_per_eu(OCC, OCC))) ric_kernel(SolveArgs a, int N, int cap) {
   extern __shared__ __attribute__((aligned(16))) double ric_sm[];
@@ -1219,7 +1258,7 @@ __global__ void __launch_bounds__(RT) __attribute__((amdgpu_waves_per_eu(OCC, OC
     if (threadIdx.x == 0) b = atomicAdd(a.work, 1);
     b = __builtin_amdgcn_readfirstlane(b);
     if (b >= a.B) break;
-    ric_solve<VAR, 1, OCC == 2 ? 2 : 3, true, NC, CAPC>(a, N, (int64_t)b, ric_sm, ric_sm + L.RM, cap, kw,
+    ric_solve<VAR, 1, OCC == 2 ? 2 : kRing1Wave, true, NC, CAPC>(a, N, (int64_t)b, ric_sm, ric_sm + L.RM, cap, kw,
                                                          kw + ric_kws_doubles(N));
     __syncthreads();
   }
