@@ -34,6 +34,8 @@
 #include <math.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "hmpc_internal.h"
 #include "hmpc_model.h"
 
@@ -42,6 +44,16 @@ namespace hmpc {
 namespace {
 
 constexpr int RT = 64;   // one wavefront per workgroup
+// MRHS (speculative candidate columns): 0 off, 1 in the
+// one-wave-per-SIMD kernels (three-deep ring), 2 in every main-pass kernel
+#ifndef HMPC_RIC_MRHS
+#define HMPC_RIC_MRHS 2
+#endif
+#ifndef HMPC_RIC_NSC
+#define HMPC_RIC_NSC 16
+#endif
+constexpr int kNSC = HMPC_RIC_MRHS ? HMPC_RIC_NSC : 0;   // candidate cache slots per workgroup (<= 64)
+constexpr int kMRK = 4;                         // right-hand sides per sweep pair (DPP rows)
 
 // LDS layout (in doubles) for a runtime horizon N and active-set capacity cap
 // (R in LDS only when r_lds).
@@ -192,6 +204,9 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
   double* cbv = sm + L.CB;
   double* sdg = sm + L.SD;
   double* un = sm + L.U0;
+  constexpr bool kMR = ENT == 1 && ZC && (HMPC_RIC_MRHS >= 2 || (HMPC_RIC_MRHS == 1 && RING != 2));
+  // MRHS candidate columns: after the cached active columns S (cap x NV)
+  [[maybe_unused]] double* gcache = kMR ? scw + (int64_t)cap * NV : nullptr;
 
 #ifdef HMPC_STAMPS
   long long rst_[16] = {0};
@@ -536,18 +551,29 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
   };
   // jt (uniform): the last stage where the right-hand side NB is nonzero --
   // the backward sweep starts there (lam_{jt+1} = 0, mu_j = 0 beyond it)
-  auto hinv = [&](double* dst, int jt) __attribute__((always_inline)) {
+  // hinv_g(MR, ...): MR = std::false_type: dst = H^-1 NB as described above.
+  // MR = std::true_type (speculative candidate columns, MRHS): up to 4
+  // right-hand sides at once, one per 16-lane DPP row -- every broadcast and
+  // row shift of the sweeps acts within a row, so row r runs the same
+  // recursion on its own vector for free.  Row r's right-hand side, its mu
+  // scratch and its result all live in one global column (colb: this lane's
+  // row's column; the backward sweep overwrites n_j with mu_j after reading
+  // it, the forward sweep w_k with u_k), rows >= nr idle (rowok false).
+  auto hinv_g = [&](auto MRt, double* dst, int jt, double* colb, bool rowok, int nr, int s0, int s1,
+                    int s2, int s3) __attribute__((always_inline)) {
+    constexpr bool MR = decltype(MRt)::value;
+    const int lr = MR ? (lane & 15) : lane;   // lane within its row
     // (lane constants made here, per call: not live across the active set)
     // per-lane constants of the A maps (see the shift comments below)
-    const double gA = (lane >= 6 && lane <= 8) || lane == 11 ? dt : 0.0;   // bwd s6, fixed
-    const double gB = (lane == 9 || lane == 10) ? dt : 0.0;                // bwd s6, * cos
-    const double gC = lane == 9 ? -dt : 0.0;                               // bwd s5, * sin
-    const double gD = lane == 10 ? dt : 0.0;                               // bwd s7, * sin
-    const double fA = lane < 3 || lane == 5 ? dt : 0.0;                    // fwd s6, fixed
-    const double fB = (lane == 3 || lane == 4) ? dt : 0.0;                 // fwd s6, * cos
-    const double fC = lane == 3 ? dt : 0.0;                                // fwd s7, * sin
-    const double fD = lane == 4 ? -dt : 0.0;                               // fwd s5, * sin
-    const int c6 = lane < 6 ? lane : 0;
+    const double gA = (lr >= 6 && lr <= 8) || lr == 11 ? dt : 0.0;   // bwd s6, fixed
+    const double gB = (lr == 9 || lr == 10) ? dt : 0.0;                // bwd s6, * cos
+    const double gC = lr == 9 ? -dt : 0.0;                               // bwd s5, * sin
+    const double gD = lr == 10 ? dt : 0.0;                               // bwd s7, * sin
+    const double fA = lr < 3 || lr == 5 ? dt : 0.0;                    // fwd s6, fixed
+    const double fB = (lr == 3 || lr == 4) ? dt : 0.0;                 // fwd s6, * cos
+    const double fC = lr == 3 ? dt : 0.0;                                // fwd s7, * sin
+    const double fD = lr == 4 ? -dt : 0.0;                               // fwd s5, * sin
+    const int c6 = lr < 6 ? lr : 0;
     // force map rows 6..8 of B_k = dtm (3f: I; 2f: Rz(psi)') as per-lane
     // coefficients P + Q cos + S sin, branch-free:
     //   k*[r] (backward, lane c < 6):  B[6+r][c]
@@ -555,20 +581,20 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
     double kP[3], kQ_[3], kS[3], rP[3], rQ[3], rS[3];
   #pragma unroll
     for (int r = 0; r < 3; ++r) {
-      const double on_b = lane == r ? dtm : 0.0, on_f = lane == 6 + r ? dtm : 0.0;
+      const double on_b = lr == r ? dtm : 0.0, on_f = lr == 6 + r ? dtm : 0.0;
       if constexpr (VAR == 3) {
         kP[r] = on_b; kQ_[r] = 0.0; kS[r] = 0.0;
         rP[r] = on_f; rQ[r] = 0.0; rS[r] = 0.0;
       } else {   // Rz' = [[c, -s, 0], [s, c, 0], [0, 0, 1]]
         kP[r] = r == 2 ? on_b : 0.0;
         kQ_[r] = r < 2 ? on_b : 0.0;
-        kS[r] = r == 0 ? (lane == 1 ? -dtm : 0.0) : (r == 1 ? (lane == 0 ? dtm : 0.0) : 0.0);
-        rP[r] = r == 2 ? (lane == 8 ? dtm : 0.0) : 0.0;
+        kS[r] = r == 0 ? (lr == 1 ? -dtm : 0.0) : (r == 1 ? (lr == 0 ? dtm : 0.0) : 0.0);
+        rP[r] = r == 2 ? (lr == 8 ? dtm : 0.0) : 0.0;
         rQ[r] = r < 2 ? on_f : 0.0;   // column r of row r: cos
-        rS[r] = r == 0 ? (lane == 7 ? dtm : 0.0) : (r == 1 ? (lane == 6 ? -dtm : 0.0) : 0.0);
+        rS[r] = r == 0 ? (lr == 7 ? dtm : 0.0) : (r == 1 ? (lr == 6 ? -dtm : 0.0) : 0.0);
       }
     }
-    const double m911 = (lane >= 9 && lane < 12) ? 1.0 : 0.0;
+    const double m911 = (lr >= 9 && lr < 12) ? 1.0 : 0.0;
     auto load_b = [&](int j, BwdL& d) __attribute__((always_inline)) {
       d.cp = cs[2 * j];
       d.sp = cs[2 * j + 1];
@@ -576,8 +602,9 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
       d.b0 = bw[18 * j + c6];
       d.b1 = bw[18 * j + 6 + c6];
       d.b2 = bw[18 * j + 12 + c6];
-      d.n = nb[6 * j + c6];
-      const double* kcol = km + 72 * j + (lane < 12 ? lane : 0);
+      if constexpr (MR) d.n = colb[6 * j + c6];
+      else d.n = nb[6 * j + c6];
+      const double* kcol = km + 72 * j + (lr < 12 ? lr : 0);
   #pragma unroll
       for (int c = 0; c < 6; ++c) d.kc[c] = kcol[12 * c];
       asm volatile("" ::: "memory");   // issue here, two steps ahead of the use
@@ -585,11 +612,12 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
     auto load_f = [&](int k, FwdL& d) __attribute__((always_inline)) {
       d.cp = cs[2 * k];
       d.sp = cs[2 * k + 1];
-      d.w = mu_[6 * k + c6];
+      if constexpr (MR) d.w = colb[6 * k + c6];
+      else d.w = mu_[6 * k + c6];
       const double* krow = km + 72 * k + 12 * c6;
   #pragma unroll
       for (int c = 0; c < 12; ++c) d.kr[c] = krow[c];
-      const int rr = (lane >= 9 && lane < 12) ? lane - 9 : 0;
+      const int rr = (lr >= 9 && lr < 12) ? lr - 9 : 0;
   #pragma unroll
       for (int c = 0; c < 6; ++c) d.br[c] = bw[18 * k + 6 * rr + c];
       asm volatile("" ::: "memory");   // issue here, two steps ahead of the use
@@ -619,9 +647,13 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
           bc = fma(k6, rdlane(li, 6), fma(k7, rdlane(li, 7), k8 * rdlane(li, 8))) +
                fma(d.b0, rdlane(li, 9), fma(d.b1, rdlane(li, 10), d.b2 * rdlane(li, 11)));
         }
-        const bool fr = lane >= 3 || (d.st != 0.0 && !(VAR == 2 && lane == 1));
+        const bool fr = lr >= 3 || (d.st != 0.0 && !(VAR == 2 && lr == 1));
         const double m = fr ? d.n - bc : d.n;
-        if (lane < 6) mu_[6 * j + lane] = m;
+        if constexpr (MR) {
+          if (lr < 6 && rowok) colb[6 * j + lr] = m;
+        } else {
+          if (lane < 6) mu_[6 * j + lane] = m;
+        }
         if (j == 0) return;
         // (A'lam)[i]: lanes 6..8 += dt lam[i-6]; 9 += dt (c lam3 - s lam4);
         // 10 += dt (s lam3 + c lam4); 11 += dt lam5
@@ -641,7 +673,7 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
           a1 = fma(d.kc[4], rdlane(m, 4), a1);
           a2 = fma(d.kc[5], rdlane(m, 5), a2);
         }
-        li = lane < 12 ? (a0 + a1) + a2 : 0.0;
+        li = lr < 12 ? (a0 + a1) + a2 : 0.0;
       };
       // (loads are unconditional -- out-of-range steps reload stage 0 -- so
       // that the vmcnt/lgkmcnt waits stay counted, not drained)
@@ -688,16 +720,24 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
         }
       }
     }
-    for (int i = 6 * (jt + 1) + lane; i < NV; i += RT) mu_[i] = 0.0;
-    wsync();
+    if constexpr (MR) {
+      gsync();   // every row's mu_j (global) visible to the lanes of the stage step
+    } else {
+      for (int i = 6 * (jt + 1) + lane; i < NV; i += RT) mu_[i] = 0.0;
+      wsync();
+    }
     // ---- w_j = G_j^-1 mu_j = Dinv'(Dinv mu_j) (lane-per-stage; 0 beyond jt)
-    for (int j = lane; j <= jt; j += RT) {
+    const int nitem = (MR ? nr : 1) * (jt + 1);
+    for (int it = lane; it < nitem; it += RT) {
+      const int r_ = MR ? it / (jt + 1) : 0, j = it - r_ * (jt + 1);
+      double* mcol = mu_;
+      if constexpr (MR) mcol = gcache + (int64_t)(r_ == 0 ? s0 : r_ == 1 ? s1 : r_ == 2 ? s2 : s3) * NV;
       double mv[6], y[6], w[6], g[21];
       const double* gj = gi + 21 * j;
 #pragma unroll
       for (int e = 0; e < 21; ++e) g[e] = gj[e];
 #pragma unroll
-      for (int c = 0; c < 6; ++c) mv[c] = mu_[6 * j + c];
+      for (int c = 0; c < 6; ++c) mv[c] = mcol[6 * j + c];
 #pragma unroll
       for (int c = 0; c < 6; ++c) {   // y = Dinv mu (lower)
         double s = 0.0;
@@ -713,9 +753,10 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
         w[c] = s;
       }
 #pragma unroll
-      for (int c = 0; c < 6; ++c) mu_[6 * j + c] = w[c];
+      for (int c = 0; c < 6; ++c) mcol[6 * j + c] = w[c];
     }
-    wsync();
+    if constexpr (MR) gsync();
+    else wsync();
     // ---- forward sweep
     {
       double xi = 0.0;   // x_k[lane]
@@ -738,7 +779,11 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
           }
         }
         const double u = a0 + a1;
-        if (lane < 6) dst[6 * k + lane] = u;
+        if constexpr (MR) {
+          if (lr < 6 && rowok) colb[6 * k + lr] = u;
+        } else {
+          if (lane < 6) dst[6 * k + lane] = u;
+        }
         // (A x)[i]: lanes 0..2 += dt x[i+6]; 3 += dt (c x9 + s x10);
         // 4 += dt (c x10 - s x9); 5 += dt x11
         const double s6 = row_shift<6>(xi), s5 = row_shift<5>(xi), s7 = row_shift<7>(xi);
@@ -770,7 +815,7 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
           b1 = fma(r4, rdlane(u, 4), b1);
           b2 = fma(r5, rdlane(u, 5), b2);
         }
-        xi = lane < 12 ? (b0 + b1) + b2 : 0.0;
+        xi = lr < 12 ? (b0 + b1) + b2 : 0.0;
       };
       if constexpr (RING >= 4) {
         FwdL R[RING];
@@ -815,7 +860,11 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
         }
       }
     }
-    wsync();
+    if constexpr (MR) gsync();
+    else wsync();
+  };
+  auto hinv = [&](double* dst, int jt) __attribute__((always_inline)) {
+    hinv_g(std::false_type{}, dst, jt, nullptr, false, 1, 0, 0, 0, 0);
   };
   // sum over all NV entries of X .* Y (lane-per-stage), wave-uniform
   auto vdot = [&](const double* X, const double* Y) -> double {
@@ -907,6 +956,10 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
     return (sl == 0 ? -X[v] : X[v]) + mu * X[6 * k + 2];
   };
 
+  // MRHS candidate cache (global, after the active columns): lane t < kNSC
+  // holds the id whose s = H^-1 n_id sits in slot t (-1: empty)
+  [[maybe_unused]] int cid = -1;
+  [[maybe_unused]] int cnext = 0;
   bool done = status != ST_SOLVED;
   while (!done) {
     RS_T(t_scan);
@@ -945,6 +998,8 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
         }
       }
     }
+    [[maybe_unused]] const double lbest = best;   // this stage's most violated (MRHS candidates)
+    [[maybe_unused]] const int lbid = bid;
     wave_argmin(best, bid);
     RS_ACC(4, t_scan);
     if (!(best < -kTol)) break;   // primal feasible: optimal
@@ -959,7 +1014,67 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
       for (int c = 0; c < 6; ++c) nb[6 * j + c] = acc[c];
     }
     rsync();
-    hinv(sv, stage_top(p));       // s = H^-1 n_p
+    if constexpr (kMR) {
+      // s = H^-1 n_p from the candidate cache, or by one multi-RHS sweep pair
+      // that also fills the cache for the next most violated constraints of
+      // other stages (MRHS)
+      const uint64_t hit = __ballot(lane < kNSC && cid == p);
+      if (hit) {
+        const double* col = gcache + (int64_t)__builtin_ctzll(hit) * NV;
+        for (int i = lane; i < NV; i += RT) sv[i] = col[i];
+        wsync();
+      } else {
+        // candidates: each stage's most violated constraint (lanes < N), not
+        // p, not cached already; the most violated of those first
+        bool cached = false;
+        for (int t = 0; t < kNSC; ++t) cached = cached || (__builtin_amdgcn_readlane(cid, t) == lbid);
+        double bl = (lane < N && lbest < -kTol && lbid != p && !cached) ? lbest : INFINITY;
+        int ids[kMRK], sl[kMRK];
+        ids[0] = p;
+        int nr = 1, jt = stage_top(p);
+#pragma unroll
+        for (int r = 1; r < kMRK; ++r) {
+          double b2 = bl;
+          int i2 = lbid;
+          wave_argmin(b2, i2);
+          if (!(b2 < -kTol)) break;
+          const int q2 = uni(i2);
+          if (lbid == q2) bl = INFINITY;
+          ids[r] = q2;
+          jt = max(jt, stage_top(q2));
+          nr = r + 1;
+        }
+        for (int r = 0; r < kMRK; ++r) {   // cache slots, round robin
+          if (r < nr) {
+            sl[r] = cnext;
+            if (lane == cnext) cid = ids[r];
+            cnext = cnext + 1 == kNSC ? 0 : cnext + 1;
+          } else {
+            sl[r] = sl[0];
+          }
+        }
+        // right-hand sides n_q into their columns
+        for (int r = 0; r < nr; ++r) {
+          double* col = gcache + (int64_t)sl[r] * NV;
+          for (int j = lane; j < N; j += RT) {
+            double acc[6] = {0, 0, 0, 0, 0, 0};
+            add_coef(ids[r], j, 1.0, acc);
+#pragma unroll
+            for (int c = 0; c < 6; ++c) col[6 * j + c] = acc[c];
+          }
+        }
+        gsync();
+        const int row = lane >> 4;
+        const int myslot = row == 0 ? sl[0] : row == 1 ? sl[1] : row == 2 ? sl[2] : sl[3];
+        hinv_g(std::true_type{}, sv, jt, gcache + (int64_t)myslot * NV, row < nr, nr, sl[0], sl[1], sl[2],
+               sl[3]);
+        const double* col = gcache + (int64_t)sl[0] * NV;
+        for (int i = lane; i < NV; i += RT) sv[i] = col[i];
+        wsync();
+      }
+    } else {
+      hinv(sv, stage_top(p));       // s = H^-1 n_p
+    }
     const double sn = vdot(nb, sv);
     const double szd = zdot(sv);
     if (lane < N) zd[lane] = szd;
@@ -1326,16 +1441,19 @@ RicCfg ric_config(int N) {
 
 int ric_qcap(int N) { return ric_config(N).cap; }
 int ric_occ(int N) { return ric_config(N).occ; }
+#ifndef HMPC_RIC_STATIC20
+#define HMPC_RIC_STATIC20 1   // 0: configs[3]'s N = 20 on the runtime-N kernel (A/B)
+#endif
 int ric_static_n(int N) {
   const RicCfg c = ric_config(N);
   if (N == 60 && c.occ == 1 && c.cap == 47) return 60;
-  if (N == 20 && c.occ == 2 && c.cap == 38) return 20;
+  if (HMPC_RIC_STATIC20 && N == 20 && c.occ == 2 && c.cap == 38) return 20;
   return 0;
 }
 
 // K / Dinv of every stage, then the cached columns H^-1 n_a (capacity x NV)
 int64_t ric_kws_stride(int N) {
-  return ric_kws_doubles(N) + ((((int64_t)ric_qcap(N) * 6 * N) + 15) & ~(int64_t)15);
+  return ric_kws_doubles(N) + (((((int64_t)ric_qcap(N) + kNSC) * 6 * N) + 15) & ~(int64_t)15);
 }
 
 int64_t ric_rws_stride(int N) {
