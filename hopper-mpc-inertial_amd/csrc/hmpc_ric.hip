@@ -49,6 +49,9 @@ constexpr int RT = 64;   // one wavefront per workgroup
 #ifndef HMPC_RIC_MRHS
 #define HMPC_RIC_MRHS 2
 #endif
+#ifndef HMPC_RIC_MRL
+#define HMPC_RIC_MRL 1   // MRHS columns in LDS where they fit (A/B: 0)
+#endif
 #ifndef HMPC_RIC_NSC
 #define HMPC_RIC_NSC 16
 #endif
@@ -162,7 +165,10 @@ __device__ __forceinline__ void vset(double (&v)[ENT], int i, double x) {
   for (int e = 0; e < ENT; ++e) v[e] = (64 * e + lane == i) ? x : v[e];
 }
 
-constexpr double kZcRel = 1e-3;
+#ifndef HMPC_RIC_ZCREL
+#define HMPC_RIC_ZCREL 1e-3
+#endif
+constexpr double kZcRel = HMPC_RIC_ZCREL;
 // ZC: z = H^-1 (n_p - N_A r) as s - sum_a r_a S_a from the cached columns
 // S_a = H^-1 n_a of the active rows (scw: cap x NV, kept in active order),
 // instead of a third pair of sweeps per iteration
@@ -205,6 +211,10 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
   double* sdg = sm + L.SD;
   double* un = sm + L.U0;
   constexpr bool kMR = ENT == 1 && ZC && (HMPC_RIC_MRHS >= 2 || (HMPC_RIC_MRHS == 1 && RING != 2));
+  // ... with its four columns in LDS (SV, ZV, MU and the union's 568-double
+  // Riccati scratch, all dead during the s sweep pair; 6N <= 568 for N <= 64)
+  constexpr bool kMRL = kMR && HMPC_RIC_MRL;
+  static_assert(6 * kRicNmax <= 568, "an MRHS column must fit the union's Riccati scratch");
   // MRHS candidate columns: after the cached active columns S (cap x NV)
   [[maybe_unused]] double* gcache = kMR ? scw + (int64_t)cap * NV : nullptr;
 
@@ -552,15 +562,16 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
   // jt (uniform): the last stage where the right-hand side NB is nonzero --
   // the backward sweep starts there (lam_{jt+1} = 0, mu_j = 0 beyond it)
   // hinv_g(MR, ...): MR = std::false_type: dst = H^-1 NB as described above.
-  // MR = std::true_type (speculative candidate columns, MRHS): up to 4
+  // MR = std::true_type (speculative candidate columns, MRHS; c0..c3 = the
+  // rows' columns): up to 4
   // right-hand sides at once, one per 16-lane DPP row -- every broadcast and
   // row shift of the sweeps acts within a row, so row r runs the same
   // recursion on its own vector for free.  Row r's right-hand side, its mu
   // scratch and its result all live in one global column (colb: this lane's
   // row's column; the backward sweep overwrites n_j with mu_j after reading
   // it, the forward sweep w_k with u_k), rows >= nr idle (rowok false).
-  auto hinv_g = [&](auto MRt, double* dst, int jt, double* colb, bool rowok, int nr, int s0, int s1,
-                    int s2, int s3) __attribute__((always_inline)) {
+  auto hinv_g = [&](auto MRt, double* dst, int jt, double* colb, bool rowok, int nr, double* c0, double* c1,
+                    double* c2, double* c3) __attribute__((always_inline)) {
     constexpr bool MR = decltype(MRt)::value;
     const int lr = MR ? (lane & 15) : lane;   // lane within its row
     // (lane constants made here, per call: not live across the active set)
@@ -731,7 +742,7 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
     for (int it = lane; it < nitem; it += RT) {
       const int r_ = MR ? it / (jt + 1) : 0, j = it - r_ * (jt + 1);
       double* mcol = mu_;
-      if constexpr (MR) mcol = gcache + (int64_t)(r_ == 0 ? s0 : r_ == 1 ? s1 : r_ == 2 ? s2 : s3) * NV;
+      if constexpr (MR) mcol = r_ == 0 ? c0 : r_ == 1 ? c1 : r_ == 2 ? c2 : c3;
       double mv[6], y[6], w[6], g[21];
       const double* gj = gi + 21 * j;
 #pragma unroll
@@ -864,7 +875,7 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
     else wsync();
   };
   auto hinv = [&](double* dst, int jt) __attribute__((always_inline)) {
-    hinv_g(std::false_type{}, dst, jt, nullptr, false, 1, 0, 0, 0, 0);
+    hinv_g(std::false_type{}, dst, jt, nullptr, false, 1, nullptr, nullptr, nullptr, nullptr);
   };
   // sum over all NV entries of X .* Y (lane-per-stage), wave-uniform
   auto vdot = [&](const double* X, const double* Y) -> double {
@@ -1053,24 +1064,49 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
             sl[r] = sl[0];
           }
         }
-        // right-hand sides n_q into their columns
-        for (int r = 0; r < nr; ++r) {
-          double* col = gcache + (int64_t)sl[r] * NV;
-          for (int j = lane; j < N; j += RT) {
-            double acc[6] = {0, 0, 0, 0, 0, 0};
-            add_coef(ids[r], j, 1.0, acc);
-#pragma unroll
-            for (int c = 0; c < 6; ++c) col[6 * j + c] = acc[c];
-          }
-        }
-        gsync();
         const int row = lane >> 4;
-        const int myslot = row == 0 ? sl[0] : row == 1 ? sl[1] : row == 2 ? sl[2] : sl[3];
-        hinv_g(std::true_type{}, sv, jt, gcache + (int64_t)myslot * NV, row < nr, nr, sl[0], sl[1], sl[2],
-               sl[3]);
-        const double* col = gcache + (int64_t)sl[0] * NV;
-        for (int i = lane; i < NV; i += RT) sv[i] = col[i];
-        wsync();
+        if constexpr (kMRL) {
+          // the four columns in LDS vectors that are dead during this sweep
+          // pair: SV (row 0, so s lands in place), ZV, MU and the union's
+          // Riccati scratch (568 >= 6N doubles); then to their cache slots
+          auto colr = [&](int r) -> double* { return r == 0 ? sv : r == 1 ? zv : r == 2 ? mu_ : un; };
+          for (int r = 0; r < nr; ++r) {
+            double* col = colr(r);
+            for (int j = lane; j < N; j += RT) {
+              double acc[6] = {0, 0, 0, 0, 0, 0};
+              add_coef(ids[r], j, 1.0, acc);
+#pragma unroll
+              for (int c = 0; c < 6; ++c) col[6 * j + c] = acc[c];
+            }
+          }
+          wsync();
+          hinv_g(std::true_type{}, sv, jt, colr(row), row < nr, nr, sv, zv, mu_, un);
+          for (int r = 0; r < nr; ++r) {
+            const double* col = colr(r);
+            double* gc = gcache + (int64_t)sl[r] * NV;
+            for (int i = lane; i < NV; i += RT) gc[i] = col[i];
+          }
+          gsync();
+        } else {
+          // right-hand sides n_q into their cache columns (global)
+          for (int r = 0; r < nr; ++r) {
+            double* col = gcache + (int64_t)sl[r] * NV;
+            for (int j = lane; j < N; j += RT) {
+              double acc[6] = {0, 0, 0, 0, 0, 0};
+              add_coef(ids[r], j, 1.0, acc);
+#pragma unroll
+              for (int c = 0; c < 6; ++c) col[6 * j + c] = acc[c];
+            }
+          }
+          gsync();
+          const int myslot = row == 0 ? sl[0] : row == 1 ? sl[1] : row == 2 ? sl[2] : sl[3];
+          hinv_g(std::true_type{}, gcache, jt, gcache + (int64_t)myslot * NV, row < nr, nr,
+                 gcache + (int64_t)sl[0] * NV, gcache + (int64_t)sl[1] * NV, gcache + (int64_t)sl[2] * NV,
+                 gcache + (int64_t)sl[3] * NV);
+          const double* col = gcache + (int64_t)sl[0] * NV;
+          for (int i = lane; i < NV; i += RT) sv[i] = col[i];
+          wsync();
+        }
       }
     } else {
       hinv(sv, stage_top(p));       // s = H^-1 n_p

@@ -1,0 +1,17 @@
+# round-3 GPU call T: MRHS columns in LDS for every Riccati main pass
+# (libhmpc_mrl.so: SV, ZV, MU, union scratch) vs global columns (libhmpc.so),
+# and the cached-column z fallback threshold (zc6 / zc9: 1e-6 / 1e-9 instead of 1e-3)
+set -o pipefail
+mkdir -p gpurun_out
+for lib in libhmpc_mrl.so libhmpc_zc6.so libhmpc_zc9.so; do
+  HMPC_LIB=$PWD/hopper-mpc-inertial_amd/$lib timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/test_gpu_riccati_stress.py tests/test_gpu_parity.py tests/test_gpu_dist.py tests/test_gpu_n60.py tests/test_gpu_overflow.py tests/test_gpu_wide.py > gpurun_out/mrl_tests.log 2>&1; rc=$?; echo "$lib tests rc $rc: $(tail -n 1 gpurun_out/mrl_tests.log)"
+  [ $rc -eq 0 ] || { grep -B3 -A25 "Error\|assert" gpurun_out/mrl_tests.log | head -40; }
+done
+for rep in 1 2; do
+  for lib in libhmpc.so libhmpc_mrl.so libhmpc_zc6.so libhmpc_zc9.so; do
+    for cfg in "--N 60 --straight --batch 4096" "--N 20 --straight --mu-sweep --global-batch 262144"; do
+      HMPC_LIB=$PWD/hopper-mpc-inertial_amd/$lib timeout -k 10 200 python -u bench.py $cfg --steps 20 --warmup 5 --cpu-seconds 0 > gpurun_out/b.json 2>gpurun_out/b.err || { tail -n 5 gpurun_out/b.err; exit 1; }
+      python -c "import json;d=json.load(open('gpurun_out/b.json'));print('$lib', '$cfg'[:7], round(d['value']/1e6,4), 'M/s', round(d['roofline']['kernel_ms'],3), 'ms')"
+    done
+  done
+done
