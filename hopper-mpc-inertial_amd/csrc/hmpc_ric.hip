@@ -52,6 +52,9 @@ constexpr int RT = 64;   // one wavefront per workgroup
 #ifndef HMPC_RIC_MRL
 #define HMPC_RIC_MRL 1   // MRHS columns in LDS where they fit (A/B: 0)
 #endif
+#ifndef HMPC_RIC_UNIFY
+#define HMPC_RIC_UNIFY 1   // single-RHS sweeps through the MRHS body too (A/B: 0)
+#endif
 #ifndef HMPC_RIC_NSC
 #define HMPC_RIC_NSC 16
 #endif
@@ -875,7 +878,16 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
     else wsync();
   };
   auto hinv = [&](double* dst, int jt) __attribute__((always_inline)) {
-    hinv_g(std::false_type{}, dst, jt, nullptr, false, 1, nullptr, nullptr, nullptr, nullptr);
+    if constexpr (ENT == 1 && ZC && HMPC_RIC_MRHS && HMPC_RIC_MRL && HMPC_RIC_UNIFY) {
+      // one sweep body in the kernel: the MRHS form with a single row, its
+      // column the destination (NB copied in first; dst is SV, ZV or VV)
+      for (int i = lane; i < NV; i += RT) dst[i] = nb[i];
+      wsync();
+      double* const c1 = dst == zv ? sv : zv;   // rows >= 1 idle: any other LDS vector
+      hinv_g(std::true_type{}, dst, jt, (lane >> 4) == 0 ? dst : c1, (lane >> 4) == 0, 1, dst, c1, c1, c1);
+    } else {
+      hinv_g(std::false_type{}, dst, jt, nullptr, false, 1, nullptr, nullptr, nullptr, nullptr);
+    }
   };
   // sum over all NV entries of X .* Y (lane-per-stage), wave-uniform
   auto vdot = [&](const double* X, const double* Y) -> double {
