@@ -1410,6 +1410,11 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
 #define HMPC_RIC_RING1 3
 #endif
 constexpr int kRing1Wave = HMPC_RIC_RING1;
+// ... and at 2 waves/SIMD (register budget 256)
+#ifndef HMPC_RIC_RING2
+#define HMPC_RIC_RING2 2
+#endif
+constexpr int kRing2Wave = HMPC_RIC_RING2;
 template <int VAR, int OCC, int NC = 0, int CAPC = 0>
 __global__ void __launch_bounds__(RT) __attribute__((amdgpu_waves_per_eu(OCC, OCC))) ric_kernel(SolveArgs a, int N, int cap) {
   extern __shared__ __attribute__((aligned(16))) double ric_sm[];
@@ -1421,7 +1426,7 @@ __global__ void __launch_bounds__(RT) __attribute__((amdgpu_waves_per_eu(OCC, OC
     if (threadIdx.x == 0) b = atomicAdd(a.work, 1);
     b = __builtin_amdgcn_readfirstlane(b);
     if (b >= a.B) break;
-    ric_solve<VAR, 1, OCC == 2 ? 2 : kRing1Wave, true, NC, CAPC>(a, N, (int64_t)b, ric_sm, ric_sm + L.RM, cap, kw,
+    ric_solve<VAR, 1, OCC == 2 ? kRing2Wave : kRing1Wave, true, NC, CAPC>(a, N, (int64_t)b, ric_sm, ric_sm + L.RM, cap, kw,
                                                          kw + ric_kws_doubles(N));
     __syncthreads();
   }
@@ -1499,7 +1504,8 @@ int ric_static_n(int N) {
   return 0;
 }
 
-// K / Dinv of every stage, then the cached columns H^-1 n_a (capacity x NV)
+// K / Dinv of every stage, then the cached columns H^-1 n_a (capacity x NV),
+// then the MRHS candidate columns (kNSC x NV)
 int64_t ric_kws_stride(int N) {
   return ric_kws_doubles(N) + (((((int64_t)ric_qcap(N) + kNSC) * 6 * N) + 15) & ~(int64_t)15);
 }
