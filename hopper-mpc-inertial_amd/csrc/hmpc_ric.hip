@@ -55,6 +55,9 @@ constexpr int RT = 64;   // one wavefront per workgroup
 #ifndef HMPC_RIC_UNIFY
 #define HMPC_RIC_UNIFY 1   // single-RHS sweeps through the MRHS body too (A/B: 0)
 #endif
+#ifndef HMPC_RIC_ZWIDE
+#define HMPC_RIC_ZWIDE 1   // the cached-column z with a lane's entries side by side: 1 one-wave kernels, 2 all, 0 off
+#endif
 #ifndef HMPC_RIC_NSC
 #define HMPC_RIC_NSC 16
 #endif
@@ -1191,7 +1194,54 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
         }
         rsync();
         bool sweep = !ZC;
-        if constexpr (ZC) {
+        if constexpr (ZC && (HMPC_RIC_ZWIDE >= 2 || (HMPC_RIC_ZWIDE == 1 && RING != 2))) {
+          // z = s - S r streamed column by column, each lane's ZE entries
+          // i = i0 + lane + 64 e side by side: 4 x ZE independent loads in flight
+          // per lane per batch of 4 columns (the latency of the L2/MALL-resident
+          // columns, not the FMAs, bounds this phase)
+          constexpr int ZE = NC > 0 ? (6 * NC + RT - 1) / RT : (RING == 2 ? 2 : 6);
+          for (int i0 = 0; i0 < NV; i0 += RT * ZE) {
+            double za[ZE], zb2[ZE];
+            const double* sc[ZE];
+#pragma unroll
+            for (int e = 0; e < ZE; ++e) {
+              const int i = i0 + lane + RT * e, ic = i < NV ? i : 0;
+              sc[e] = scw + ic;
+              za[e] = sv[ic];
+              zb2[e] = 0.0;
+            }
+            int a0 = 0;
+            for (; a0 + 4 <= q; a0 += 4) {
+              const double r0 = cbv[a0], r1 = cbv[a0 + 1], r2 = cbv[a0 + 2], r3 = cbv[a0 + 3];
+              double c[ZE][4];
+#pragma unroll
+              for (int e = 0; e < ZE; ++e) {
+#pragma unroll
+                for (int t = 0; t < 4; ++t) c[e][t] = sc[e][(int64_t)(a0 + t) * NV];
+              }
+#pragma unroll
+              for (int e = 0; e < ZE; ++e) {
+                za[e] = fma(-r0, c[e][0], za[e]);
+                zb2[e] = fma(-r1, c[e][1], zb2[e]);
+                za[e] = fma(-r2, c[e][2], za[e]);
+                zb2[e] = fma(-r3, c[e][3], zb2[e]);
+              }
+            }
+            for (; a0 < q; ++a0) {
+              const double r0 = cbv[a0];
+#pragma unroll
+              for (int e = 0; e < ZE; ++e) za[e] = fma(-r0, sc[e][(int64_t)a0 * NV], za[e]);
+            }
+#pragma unroll
+            for (int e = 0; e < ZE; ++e) {
+              const int i = i0 + lane + RT * e;
+              if (i < NV) zv[i] = za[e] + zb2[e];
+            }
+          }
+          rsync();
+          zn = vdot(nb, zv);
+          sweep = !(zn > kZcRel * sn);
+        } else if constexpr (ZC) {
           for (int i = lane; i < NV; i += RT) {
             const double* sc = scw + i;
             double z0 = sv[i], z1 = 0.0;
