@@ -1630,12 +1630,17 @@ solve_kernel(SolveArgs a) {
 // NVM free variables: NVM-wide rows, 3 waves / SIMD) or to the full kernel,
 // by the number of stance stages of its contact schedule C (free variables
 // nf = 3N + (3f: 3, 2f: 2) x stance stages).  One thread per instance; the
-// two class lists are appended wave by wave (one atomic per wave and list):
+// two class lists are appended block by block (one atomic per block and list):
 // list A at split_list[0..B), list B at split_list[B..2B), lengths in
 // split_count[0..1] (zero at the launch; the overflow pass zeroes them).
+constexpr int kClsT = 1024;   // classify threads per block
 template <int VAR, int N, int NVM>
-__global__ void __launch_bounds__(256) classify_kernel(SolveArgs a) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+__global__ void __launch_bounds__(kClsT) classify_kernel(SolveArgs a) {
+  // (one atomic per block and list: per-wave atomics on the two counters
+  // serialised at the L2 and made this pass 25 us of a 1.3 ms step)
+  __shared__ int wc[kClsT / 64][2];
+  __shared__ int base[2];
+  const int64_t i = (int64_t)blockIdx.x * kClsT + threadIdx.x;
   const bool in = i < a.B;
   int nst = 0;
   if (in) {
@@ -1646,17 +1651,28 @@ __global__ void __launch_bounds__(256) classify_kernel(SolveArgs a) {
   const int nf = 3 * N + (VAR == 3 ? 3 : 2) * nst;
   const bool cmp = in && nf <= NVM, full = in && !cmp;
   const uint64_t mc = __ballot(cmp), mf = __ballot(full);
-  const int lane = threadIdx.x & 63;
-  const uint64_t lt = (1ull << lane) - 1;
-  int bc = 0, bf = 0;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   if (lane == 0) {
-    if (mc) bc = atomicAdd(a.split_count, __builtin_popcountll(mc));
-    if (mf) bf = atomicAdd(a.split_count + 1, __builtin_popcountll(mf));
+    wc[w][0] = __builtin_popcountll(mc);
+    wc[w][1] = __builtin_popcountll(mf);
   }
-  bc = __builtin_amdgcn_readfirstlane(bc);
-  bf = __builtin_amdgcn_readfirstlane(bf);
-  if (cmp) a.split_list[bc + __builtin_popcountll(mc & lt)] = (int32_t)i;
-  if (full) a.split_list[a.B + bf + __builtin_popcountll(mf & lt)] = (int32_t)i;
+  __syncthreads();
+  if (threadIdx.x == 0) {   // exclusive scan of the wave counts, one atomic per list
+    int tc = 0, tf = 0;
+    for (int v = 0; v < kClsT / 64; ++v) {
+      const int c = wc[v][0], f = wc[v][1];
+      wc[v][0] = tc;
+      wc[v][1] = tf;
+      tc += c;
+      tf += f;
+    }
+    base[0] = tc ? atomicAdd(a.split_count, tc) : 0;
+    base[1] = tf ? atomicAdd(a.split_count + 1, tf) : 0;
+  }
+  __syncthreads();
+  const uint64_t lt = (1ull << lane) - 1;
+  if (cmp) a.split_list[base[0] + wc[w][0] + __builtin_popcountll(mc & lt)] = (int32_t)i;
+  if (full) a.split_list[a.B + base[1] + wc[w][1] + __builtin_popcountll(mf & lt)] = (int32_t)i;
 }
 
 }  // namespace
@@ -1686,14 +1702,14 @@ bool HMPC_CAT(HMPC_CAT(launch_solve_n, HMPC_INST_N), HMPC_LAUNCH_SUFFIX)(int var
   af.list_count = nullptr;
 #if defined(HMPC_CMP_NV) && HMPC_CMP_NV > 0
   if (a.split_list && a.split_count) {   // classify, then one launch per class
-    const unsigned cb = (unsigned)((a.B + 255) / 256);
+    const unsigned cb = (unsigned)((a.B + kClsT - 1) / kClsT);
     SolveArgs ac = af;
     ac.list = a.split_list;
     ac.list_count = a.split_count;
     af.list = a.split_list + a.B;
     af.list_count = a.split_count + 1;
-    if (variant == 3) hipLaunchKernelGGL((classify_kernel<3, N, HMPC_CMP_NV>), dim3(cb), dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((classify_kernel<2, N, HMPC_CMP_NV>), dim3(cb), dim3(256), 0, s, a);
+    if (variant == 3) hipLaunchKernelGGL((classify_kernel<3, N, HMPC_CMP_NV>), dim3(cb), dim3(kClsT), 0, s, a);
+    else hipLaunchKernelGGL((classify_kernel<2, N, HMPC_CMP_NV>), dim3(cb), dim3(kClsT), 0, s, a);
     // the two classes run concurrently: the full kernel on the caller's
     // stream, the compacted one on the split stream, joined back before the
     // overflow pass (one kernel's tail fills with the other's waves)
