@@ -28,9 +28,19 @@ cmp_flags() {
     if [ "$cn" = "$1" ]; then echo "-DHMPC_CMP_NV=$cv -DHMPC_CMP_Q=$cq"; fi
   done
 }
+# register budgets (0: the compiler's) of the full and compacted one-wave kernels
+FULL_VGPR=${FULL_VGPR:-0}
+CMP_VGPR=${CMP_VGPR:-0}
+kattr() { if [ "$1" -gt 0 ]; then echo "-DHMPC_KATTR=__attribute__((amdgpu_num_vgpr($(($1 / 2)))))"; fi; }
+CMPOBJS=""
 for n in $HORIZONS; do
-  $HIPCC $FLAGS -DHMPC_INST_N=$n $(cmp_flags $n) -c ${KSRC:-csrc/hmpc_kernels.hip} -o $BDIR/hmpc_kernels_n$n.o "$@" &
+  $HIPCC $FLAGS -DHMPC_INST_N=$n $(cmp_flags $n) $([ -n "$(cmp_flags $n)" ] && kattr $FULL_VGPR) -c ${KSRC:-csrc/hmpc_kernels.hip} -o $BDIR/hmpc_kernels_n$n.o "$@" &
   pids+=($!)
+  if [ -n "$(cmp_flags $n)" ]; then   # the compacted kernel: a translation unit of its own
+    $HIPCC $FLAGS -DHMPC_INST_N=$n $(cmp_flags $n) -DHMPC_CMP_ONLY $(kattr $CMP_VGPR) -c ${KSRC:-csrc/hmpc_kernels.hip} -o $BDIR/hmpc_kernels_n${n}_cmp.o "$@" &
+    pids+=($!)
+    CMPOBJS="$CMPOBJS $BDIR/hmpc_kernels_n${n}_cmp.o"
+  fi
   while [ "$(jobs -rp | wc -l)" -ge "$JOBS" ]; do sleep 1; done
 done
 for n in $F32_HORIZONS; do
@@ -56,6 +66,7 @@ pids+=($!)
 for p in "${pids[@]}"; do wait "$p"; done
 objs=""
 for n in $HORIZONS; do objs="$objs $BDIR/hmpc_kernels_n$n.o"; done
+objs="$objs $CMPOBJS"
 for n in $F32_HORIZONS; do objs="$objs $BDIR/hmpc_kernels_n${n}_f32.o"; done
 $HIPCC --offload-arch=gfx950 -shared -fPIC $objs $BDIR/hmpc_dispatch.o $BDIR/hmpc_capi.o $BDIR/hmpc_plant.o $BDIR/hmpc_planner.o $BDIR/hmpc_cas.o $BDIR/hmpc_wide.o $BDIR/hmpc_ric.o -o $OUT.tmp
 mv $OUT.tmp $OUT

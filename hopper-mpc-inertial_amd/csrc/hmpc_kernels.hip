@@ -526,8 +526,15 @@ __device__ __forceinline__ real tri_bwd(real acc, const real* Mc, const real* ze
 #ifndef HMPC_CMP_WAVES
 #define HMPC_CMP_WAVES 3
 #endif
+// HMPC_KATTR: extra attributes of every solve_kernel in this translation unit.
+// build.sh gives the split launch's compacted kernel a translation unit of its
+// own (-DHMPC_CMP_ONLY), so each class can carry its own register budget:
+// amdgpu_num_vgpr counts VGPR pairs on gfx950 (unified VGPR/AGPR file).
+#ifndef HMPC_KATTR
+#define HMPC_KATTR
+#endif
 template <int VAR, int N, typename R, int NVM = 0, int QM = 0>
-__global__ void __launch_bounds__((Lay<N, NVM, QM>::NT),
+__global__ void HMPC_KATTR __launch_bounds__((Lay<N, NVM, QM>::NT),
                                   (NVM > 0 ? HMPC_CMP_WAVES : HMPC_WAVES_PER_EU((Lay<N, NVM, QM>::W))))
 solve_kernel(SolveArgs a) {
   static_assert(sizeof(R) == sizeof(real), "one arithmetic type per build");
@@ -1691,6 +1698,20 @@ __global__ void __launch_bounds__(kClsT) classify_kernel(SolveArgs a) {
 #ifndef HMPC_LAUNCH_SUFFIX
 #define HMPC_LAUNCH_SUFFIX
 #endif
+#if defined(HMPC_CMP_NV) && HMPC_CMP_NV > 0
+// the split's compacted kernel launches from a translation unit of its own
+// (-DHMPC_CMP_ONLY), so that its register budget (HMPC_KATTR) is its own
+bool HMPC_CAT(launch_cmp_n, HMPC_INST_N)(int variant, const SolveArgs& a, hipStream_t s);
+#endif
+#ifdef HMPC_CMP_ONLY
+bool HMPC_CAT(launch_cmp_n, HMPC_INST_N)(int variant, const SolveArgs& a, hipStream_t s) {
+  if (variant == 3)
+    hipLaunchKernelGGL((solve_kernel<3, HMPC_INST_N, real, HMPC_CMP_NV, HMPC_CMP_Q>), dim3((unsigned)a.B), dim3(64), 0, s, a);
+  else
+    hipLaunchKernelGGL((solve_kernel<2, HMPC_INST_N, real, HMPC_CMP_NV, HMPC_CMP_Q>), dim3((unsigned)a.B), dim3(64), 0, s, a);
+  return true;
+}
+#else
 bool HMPC_CAT(HMPC_CAT(launch_solve_n, HMPC_INST_N), HMPC_LAUNCH_SUFFIX)(int variant, const SolveArgs& a,
                                                                      hipStream_t s) {
   constexpr int N = HMPC_INST_N;
@@ -1721,10 +1742,7 @@ bool HMPC_CAT(HMPC_CAT(launch_solve_n, HMPC_INST_N), HMPC_LAUNCH_SUFFIX)(int var
     }
     if (variant == 3) hipLaunchKernelGGL((solve_kernel<3, N, real>), dim3((unsigned)a.B), dim3(NT), 0, s, af);
     else hipLaunchKernelGGL((solve_kernel<2, N, real>), dim3((unsigned)a.B), dim3(NT), 0, s, af);
-    if (variant == 3)
-      hipLaunchKernelGGL((solve_kernel<3, N, real, HMPC_CMP_NV, HMPC_CMP_Q>), dim3((unsigned)a.B), dim3(64), 0, s2, ac);
-    else
-      hipLaunchKernelGGL((solve_kernel<2, N, real, HMPC_CMP_NV, HMPC_CMP_Q>), dim3((unsigned)a.B), dim3(64), 0, s2, ac);
+    HMPC_CAT(launch_cmp_n, HMPC_INST_N)(variant, ac, s2);
     if (s2 != s) {
       if (hipEventRecord(a.split_join, s2) != hipSuccess) return false;
       if (hipStreamWaitEvent(s, a.split_join, 0) != hipSuccess) return false;
@@ -1764,5 +1782,6 @@ const char* HMPC_CAT(HMPC_CAT(name_solve_n, HMPC_INST_N), HMPC_LAUNCH_SUFFIX)(in
     return HMPC_NAME_CMP(2) "hmpc::solve_kernel<2, " HMPC_STR(HMPC_INST_N) ", " HMPC_STR(HMPC_REAL) ", 0, 0>";
   return "";
 }
+#endif  // HMPC_CMP_ONLY
 
 }  // namespace hmpc
