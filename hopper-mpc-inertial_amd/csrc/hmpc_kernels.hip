@@ -519,6 +519,16 @@ __device__ __forceinline__ real tri_bwd(real acc, const real* Mc, const real* ze
 #ifndef HMPC_PRIO
 #define HMPC_PRIO 1
 #endif
+// Between the split's classes: the full kernel's waves hold the small-batch
+// critical path (its instances are the longest), so they run at priority 2
+// outside the chain phases (3 inside), the compacted kernel's at 0 / 1.
+// configs[1] +1.6 %, configs[2] and B = 16384 unchanged (profiles/r03_ab.json).
+#ifndef HMPC_PRIO_CMP
+#define HMPC_PRIO_CMP 1
+#endif
+#ifndef HMPC_PRIO_FULL_BASE
+#define HMPC_PRIO_FULL_BASE 2
+#endif
 #ifndef HMPC_WAVES_PER_EU
 #define HMPC_WAVES_PER_EU(W) ((W) == 1 ? 2 : 1)
 #endif
@@ -552,6 +562,7 @@ solve_kernel(SolveArgs a) {
   long long stamp_[16] = {0};
 #endif
   HMPC_STAMP(0);
+  if constexpr (HMPC_PRIO_FULL_BASE != 0 && NVM == 0) __builtin_amdgcn_s_setprio(HMPC_PRIO_FULL_BASE);
 
   const int tid = threadIdx.x;
   // split launch (launch_solve_n<N>): block i solves the i-th instance of this
@@ -967,7 +978,7 @@ solve_kernel(SolveArgs a) {
   real wv = -hv;   // the forward sweep's accumulator (phase 4)
   __syncthreads();   // union A (XLIN/XREF/PF/S/DG) is dead from here on
   HMPC_STAMP(4);
-  if constexpr (HMPC_PRIO != 0) __builtin_amdgcn_s_setprio(3);
+  if constexpr (HMPC_PRIO != 0) __builtin_amdgcn_s_setprio(NVM > 0 ? HMPC_PRIO_CMP : 3);
 
   int status = ST_SOLVED;
   real dinv = 0.0;
@@ -1202,7 +1213,7 @@ solve_kernel(SolveArgs a) {
     if constexpr (W == 1) dinv = active_lane ? dinv : real(1);   // padding: never stepped
   }
   HMPC_STAMP(5);
-  if constexpr (HMPC_PRIO == 2) __builtin_amdgcn_s_setprio(0);
+  if constexpr (HMPC_PRIO == 2) __builtin_amdgcn_s_setprio(NVM > 0 ? 0 : HMPC_PRIO_FULL_BASE);
 
   const real* Lc = sm + L::LC;
   const real* zero = sm + L::ZR;
@@ -1542,7 +1553,7 @@ solve_kernel(SolveArgs a) {
   }
 #endif
   HMPC_STAMP(7);
-  if constexpr (HMPC_PRIO != 0) __builtin_amdgcn_s_setprio(0);
+  if constexpr (HMPC_PRIO != 0) __builtin_amdgcn_s_setprio(NVM > 0 ? 0 : HMPC_PRIO_FULL_BASE);
 
   // an overflowed instance writes nothing but its status and its place in
   // the overflow list (x_lin may be this solve's input, mpcontrol shift)
