@@ -49,6 +49,8 @@
 #include <math.h>
 #include <stdint.h>
 
+#include <stdio.h>
+#include <string>
 #include <utility>
 
 #include "hmpc_internal.h"
@@ -543,9 +545,13 @@ __device__ __forceinline__ real tri_bwd(real acc, const real* Mc, const real* ze
 #ifndef HMPC_KATTR
 #define HMPC_KATTR
 #endif
+// the widest compacted rows that fit 3 waves / SIMD (<= 168 VGPRs); a wider
+// compacted kernel (2f's 5N-wide full class) runs 2 waves like the full one
+constexpr int kCmp3W = 48;
 template <int VAR, int N, typename R, int NVM = 0, int QM = 0>
 __global__ void HMPC_KATTR __launch_bounds__((Lay<N, NVM, QM>::NT),
-                                  (NVM > 0 ? HMPC_CMP_WAVES : HMPC_WAVES_PER_EU((Lay<N, NVM, QM>::W))))
+                                  (NVM > 0 && NVM <= kCmp3W ? HMPC_CMP_WAVES
+                                   : (NVM > 0 ? 2 : HMPC_WAVES_PER_EU((Lay<N, NVM, QM>::W)))))
 solve_kernel(SolveArgs a) {
   static_assert(sizeof(R) == sizeof(real), "one arithmetic type per build");
   using L = Lay<N, NVM, QM>;
@@ -562,7 +568,8 @@ solve_kernel(SolveArgs a) {
   long long stamp_[16] = {0};
 #endif
   HMPC_STAMP(0);
-  if constexpr (HMPC_PRIO_FULL_BASE != 0 && NVM == 0) __builtin_amdgcn_s_setprio(HMPC_PRIO_FULL_BASE);
+  constexpr bool kCmpCls = NVM > 0 && NVM <= kCmp3W;   // the split's compacted class
+  if constexpr (HMPC_PRIO_FULL_BASE != 0 && !kCmpCls) __builtin_amdgcn_s_setprio(HMPC_PRIO_FULL_BASE);
 
   const int tid = threadIdx.x;
   // split launch (launch_solve_n<N>): block i solves the i-th instance of this
@@ -978,7 +985,7 @@ solve_kernel(SolveArgs a) {
   real wv = -hv;   // the forward sweep's accumulator (phase 4)
   __syncthreads();   // union A (XLIN/XREF/PF/S/DG) is dead from here on
   HMPC_STAMP(4);
-  if constexpr (HMPC_PRIO != 0) __builtin_amdgcn_s_setprio(NVM > 0 ? HMPC_PRIO_CMP : 3);
+  if constexpr (HMPC_PRIO != 0) __builtin_amdgcn_s_setprio(kCmpCls ? HMPC_PRIO_CMP : 3);
 
   int status = ST_SOLVED;
   real dinv = 0.0;
@@ -1213,7 +1220,7 @@ solve_kernel(SolveArgs a) {
     if constexpr (W == 1) dinv = active_lane ? dinv : real(1);   // padding: never stepped
   }
   HMPC_STAMP(5);
-  if constexpr (HMPC_PRIO == 2) __builtin_amdgcn_s_setprio(NVM > 0 ? 0 : HMPC_PRIO_FULL_BASE);
+  if constexpr (HMPC_PRIO == 2) __builtin_amdgcn_s_setprio(kCmpCls ? 0 : HMPC_PRIO_FULL_BASE);
 
   const real* Lc = sm + L::LC;
   const real* zero = sm + L::ZR;
@@ -1553,7 +1560,7 @@ solve_kernel(SolveArgs a) {
   }
 #endif
   HMPC_STAMP(7);
-  if constexpr (HMPC_PRIO != 0) __builtin_amdgcn_s_setprio(NVM > 0 ? 0 : HMPC_PRIO_FULL_BASE);
+  if constexpr (HMPC_PRIO != 0) __builtin_amdgcn_s_setprio(kCmpCls ? 0 : HMPC_PRIO_FULL_BASE);
 
   // an overflowed instance writes nothing but its status and its place in
   // the overflow list (x_lin may be this solve's input, mpcontrol shift)
@@ -1713,6 +1720,14 @@ __global__ void __launch_bounds__(kClsT) classify_kernel(SolveArgs a) {
 // the split's compacted kernel launches from a translation unit of its own
 // (-DHMPC_CMP_ONLY), so that its register budget (HMPC_KATTR) is its own
 bool HMPC_CAT(launch_cmp_n, HMPC_INST_N)(int variant, const SolveArgs& a, hipStream_t s);
+// 2f's full class: at most 5N free variables (3N torques + 2N stance forces;
+// f_y is fixed), so a 5N-wide compacted kernel replaces the 6N-wide full one
+// when 5N rows fit one wave (same capacity as the full kernel)
+#if 5 * HMPC_INST_N > HMPC_CMP_NV && 5 * HMPC_INST_N <= 64
+#define HMPC_FULL2F_NV (5 * HMPC_INST_N)
+#define HMPC_FULL2F_Q (Lay<HMPC_INST_N>::QMAX)
+bool HMPC_CAT(launch_full2f_n, HMPC_INST_N)(const SolveArgs& a, hipStream_t s);
+#endif
 #endif
 #ifdef HMPC_CMP_ONLY
 bool HMPC_CAT(launch_cmp_n, HMPC_INST_N)(int variant, const SolveArgs& a, hipStream_t s) {
@@ -1722,6 +1737,13 @@ bool HMPC_CAT(launch_cmp_n, HMPC_INST_N)(int variant, const SolveArgs& a, hipStr
     hipLaunchKernelGGL((solve_kernel<2, HMPC_INST_N, real, HMPC_CMP_NV, HMPC_CMP_Q>), dim3((unsigned)a.B), dim3(64), 0, s, a);
   return true;
 }
+#ifdef HMPC_FULL2F_NV
+bool HMPC_CAT(launch_full2f_n, HMPC_INST_N)(const SolveArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL((solve_kernel<2, HMPC_INST_N, real, HMPC_FULL2F_NV, HMPC_FULL2F_Q>), dim3((unsigned)a.B), dim3(64), 0,
+                     s, a);
+  return true;
+}
+#endif
 #else
 bool HMPC_CAT(HMPC_CAT(launch_solve_n, HMPC_INST_N), HMPC_LAUNCH_SUFFIX)(int variant, const SolveArgs& a,
                                                                      hipStream_t s) {
@@ -1752,7 +1774,11 @@ bool HMPC_CAT(HMPC_CAT(launch_solve_n, HMPC_INST_N), HMPC_LAUNCH_SUFFIX)(int var
       s2 = a.split_stream;
     }
     if (variant == 3) hipLaunchKernelGGL((solve_kernel<3, N, real>), dim3((unsigned)a.B), dim3(NT), 0, s, af);
+#ifdef HMPC_FULL2F_NV
+    else HMPC_CAT(launch_full2f_n, HMPC_INST_N)(af, s);
+#else
     else hipLaunchKernelGGL((solve_kernel<2, N, real>), dim3((unsigned)a.B), dim3(NT), 0, s, af);
+#endif
     HMPC_CAT(launch_cmp_n, HMPC_INST_N)(variant, ac, s2);
     if (s2 != s) {
       if (hipEventRecord(a.split_join, s2) != hipSuccess) return false;
@@ -1790,7 +1816,19 @@ const char* HMPC_CAT(HMPC_CAT(name_solve_n, HMPC_INST_N), HMPC_LAUNCH_SUFFIX)(in
   if (variant == 3)
     return HMPC_NAME_CMP(3) "hmpc::solve_kernel<3, " HMPC_STR(HMPC_INST_N) ", " HMPC_STR(HMPC_REAL) ", 0, 0>";
   if (variant == 2)
+#ifdef HMPC_FULL2F_NV
+  {
+    static const std::string name = [] {
+      char buf[256];
+      snprintf(buf, sizeof buf, "%shmpc::solve_kernel<2, %d, %s, %d, %d>", HMPC_NAME_CMP(2), HMPC_INST_N,
+               HMPC_STR(HMPC_REAL), HMPC_FULL2F_NV, HMPC_FULL2F_Q);
+      return std::string(buf);
+    }();
+    return name.c_str();
+  }
+#else
     return HMPC_NAME_CMP(2) "hmpc::solve_kernel<2, " HMPC_STR(HMPC_INST_N) ", " HMPC_STR(HMPC_REAL) ", 0, 0>";
+#endif
   return "";
 }
 #endif  // HMPC_CMP_ONLY
