@@ -1,4 +1,4 @@
-# round-3 GPU call AC: final dense build (block classify, class priorities) -- full -m gpu suite
+# round-3 GPU call AC: final dense build (block classify, class priorities, 2f 5N-wide full class) -- full -m gpu suite
 # + smoke, configs[2] / configs[1] / fp32 profiles, the default bench line
 set -o pipefail
 mkdir -p gpurun_out
