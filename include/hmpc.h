@@ -221,8 +221,9 @@ int hmpc_set_precision(hmpc_ctx* ctx, int precision);
 /* Name of the solve kernel this context's (variant, N, precision) runs on,
    as rocprofv3 demangles it, e.g. "hmpc::ric_kernel<3, 2, 0, 0>"; a split launch names
    both kernels, "hmpc::solve_kernel<3, 10, double, 48, 13> + hmpc::solve_kernel<3, 10,
-   double, 0, 0>" (the compacted one first).  Static string, "" when none.  For benchmark
-   records and profiles. */
+   double, 0, 0>" (the compacted one first; 2f's full class is the 5N-wide
+   "hmpc::solve_kernel<2, 10, double, 50, 20>").  Static string, "" when none.  For
+   benchmark records and profiles. */
 const char* hmpc_kernel_name(hmpc_ctx* ctx);
 
 /* Active-set capacity of that kernel's main pass (-1 when none): instances
