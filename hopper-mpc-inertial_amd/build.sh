@@ -68,6 +68,9 @@ objs=""
 for n in $HORIZONS; do objs="$objs $BDIR/hmpc_kernels_n$n.o"; done
 objs="$objs $CMPOBJS"
 for n in $F32_HORIZONS; do objs="$objs $BDIR/hmpc_kernels_n${n}_f32.o"; done
+# every object but the ABI/dispatch host code, for tests/test_sanitizers.py (which
+# rebuilds those two under ASan/UBSan and links the kernels as built)
+echo $objs $BDIR/hmpc_plant.o $BDIR/hmpc_planner.o $BDIR/hmpc_cas.o $BDIR/hmpc_wide.o $BDIR/hmpc_ric.o | tr ' ' '\n' > $BDIR/objs.txt
 $HIPCC --offload-arch=gfx950 -shared -fPIC $objs $BDIR/hmpc_dispatch.o $BDIR/hmpc_capi.o $BDIR/hmpc_plant.o $BDIR/hmpc_planner.o $BDIR/hmpc_cas.o $BDIR/hmpc_wide.o $BDIR/hmpc_ric.o -o $OUT.tmp
 mv $OUT.tmp $OUT
 echo "built $(pwd)/$OUT (horizons: $HORIZONS)"

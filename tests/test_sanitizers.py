@@ -40,11 +40,22 @@ def test_port_under_asan_ubsan():
 @pytest.mark.skipif(shutil.which('/opt/rocm/bin/hipcc') is None, reason='hipcc absent')
 def test_capi_argument_checks_under_asan_ubsan(tmp_path):
     pkg = os.path.join(ROOT, 'hopper-mpc-inertial_amd')
-    objs = [os.path.join(pkg, 'build', f) for f in
-            ('hmpc_kernels_n5.o', 'hmpc_kernels_n10.o', 'hmpc_kernels_n20.o', 'hmpc_kernels_n10_f32.o', 'hmpc_plant.o', 'hmpc_planner.o', 'hmpc_cas.o',
-             'hmpc_wide.o', 'hmpc_ric.o')]
-    if not all(os.path.exists(o) for o in objs):
+    # build.sh writes the kernel objects it linked into libhmpc.so (everything but the
+    # ABI and dispatch host code, rebuilt below under the sanitizers)
+    listing = os.path.join(pkg, 'build', 'objs.txt')
+
+    def _objs():
+        if not os.path.exists(listing):
+            return None
+        with open(listing) as f:
+            objs = [os.path.join(pkg, p) for p in f.read().split()]
+        return objs if objs and all(os.path.exists(o) for o in objs) else None
+
+    objs = _objs()
+    if objs is None:
         subprocess.check_call(['bash', os.path.join(pkg, 'build.sh')])
+        objs = _objs()
+    assert objs, 'build.sh wrote no object list'
     hip = '/opt/rocm/bin/hipcc'
     san = ['-Xarch_host', '-fsanitize=address', '-Xarch_host', '-fsanitize=undefined']
     flags = ['--offload-arch=gfx950', '-O1', '-g', '-std=c++17'] + san
