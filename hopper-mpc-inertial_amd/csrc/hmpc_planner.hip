@@ -135,10 +135,8 @@ __global__ void plan_peaks_kernel(PlanArgs a) {
       if (xa < xi) {
         int p = (i + (ia - 1)) / 2 + a.step_adjustment;
         if (p < 0) p += n;   // a negative numpy index counts from the end
-        if (p < 0 || p >= n) {   // numpy: IndexError when x_ref[idx_pf[kf]] is read
-          atomicOr(a.err, kErrPeakIdx);
-          p = p < 0 ? 0 : n - 1;
-        }
+        if (p < 0 || p >= n)   // numpy: IndexError only when x_ref[idx_pf[kf]] is read:
+          p = -1 - (p < 0 ? 0 : n - 1);   // kept clamped and marked (< 0), plan_rows_kernel reports it
         if (m < kMaxPeaks) pk[m++] = p;
         else atomicOr(a.err, kErrPeaks);   // the reference keeps every peak
         i = ia;
@@ -204,7 +202,11 @@ __global__ void plan_rows_kernel(PlanArgs a) {
       atomicOr(a.err, kErrFootIdx);
       kf = n_idx - 1;
     }
-    const int j = pk[kf];
+    int j = pk[kf];
+    if (j < 0) {   // a peak outside the plan (plan_peaks_kernel), read here: IndexError (:223)
+      atomicOr(a.err, kErrPeakIdx);
+      j = -1 - j;
+    }
     pf[0] = row_val(a, x0, x1, anyzero, j, 0);
     pf[1] = row_val(a, x0, x1, anyzero, j, 1);
   }

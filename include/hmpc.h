@@ -104,8 +104,12 @@ int hmpc_version(void);
    context's workspaces and counters are shared by its calls, so the context
    orders them itself: a call on a different stream than the context's last
    one first makes its stream wait for that call's completion event
-   (hipStreamWaitEvent).  Calls on one context never overlap; use one context
-   per stream for concurrent solves. */
+   (hipStreamWaitEvent).  Eager calls on one context never overlap; use one
+   context per stream for concurrent solves.  Calls enqueued while their stream
+   captures a HIP graph are outside this ordering (a replay runs whenever the
+   caller launches it): the caller orders a graph's replays against the
+   context's other streams, e.g. by synchronising the replay stream before
+   the next eager call elsewhere (hmpc_runner.Runner does). */
 int hmpc_supported_horizons(int variant, int* Ns, int cap);
 
 /* Mpc.__init__: t = MPC sampling time (s), N = horizon, m (kg), g (m/s^2),

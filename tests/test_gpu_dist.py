@@ -15,6 +15,7 @@ import socket
 
 import numpy as np
 import pytest
+from conftest import DENSE10_3F
 
 torch = pytest.importorskip('torch')
 
@@ -35,7 +36,7 @@ def _free_port():
 
 
 # name -> (horizon, --curve, global batch or 0 = PER_RANK per rank, kernel)
-WORKLOADS = {'cfg2_weak': (N, True, 0, 'hmpc::solve_kernel<3, 10, double, 48, 13> + hmpc::solve_kernel<3, 10, double, 0, 0>'),
+WORKLOADS = {'cfg2_weak': (N, True, 0, DENSE10_3F),
              'cfg3_strong': (20, False, 4097, 'hmpc::ric_kernel<3, 2, 20, 38>')}
 
 

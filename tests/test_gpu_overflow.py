@@ -14,6 +14,7 @@ really exceed the capacities it claims to cover.
 """
 import numpy as np
 import pytest
+from conftest import DENSE10_3F
 
 torch = pytest.importorskip('torch')
 
@@ -78,7 +79,7 @@ def solve_both(hm, N, inst, precision):
     return gpu, ref, kernel, cap
 
 
-@pytest.mark.parametrize('precision,kernel', [('f64', 'hmpc::solve_kernel<3, 10, double, 48, 13> + hmpc::solve_kernel<3, 10, double, 0, 0>'),
+@pytest.mark.parametrize('precision,kernel', [('f64', DENSE10_3F),
                                              ('f64_riccati', 'hmpc::ric_kernel<3, 2, 0, 0>')])
 def test_overflow_n10(hm, precision, kernel):
     N, B = 10, 48

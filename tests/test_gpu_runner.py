@@ -215,3 +215,21 @@ def test_runner_graph_replay_equals_eager(hm):
         for k in ('X_traj', 'f_hist', 'status', 'x_ref', 'pf_ref'):
             np.testing.assert_array_equal(got[k], want[k], err_msg=k)
     assert not np.array_equal(e['X_traj'], eb['X_traj'])
+
+
+def test_runner_eager_after_capture(hm):
+    """An eager run on the default stream right after a graph capture on the
+    Runner's stream, then a replay: the context's stream ordering
+    skips the capture (no wait on, or record of, a captured event), and all
+    three runs agree bit for bit."""
+    import hmpc_runner
+    B, n = 3, 8
+    r = hmpc_runner.Runner(dyn='3f', curve=False, N_run=300, N=10, batch=B)
+    g1 = r.run(n_periods=n, graph=True)    # eager on the Runner's stream, then the capture
+    e = r.run(n_periods=n)                 # eager on the default stream
+    g2 = r.run(n_periods=n, graph=True)    # replay
+    e2 = r.run(n_periods=n)
+    r.close()
+    for got in (g1, g2, e2):
+        for k in ('X_traj', 'f_hist', 'status'):
+            np.testing.assert_array_equal(got[k], e[k], err_msg=k)
