@@ -63,8 +63,9 @@ def algorithmic_bytes(N, with_mu=True):
 def algorithmic_flops(kernel, N, iters, q):
     """fp64 flops one solve needs in the algorithm the kernel runs (2 per
     FMA; DESIGN.md 5 derives each term), as a closed form over the horizon N,
-    the active-set iterations and the active-set size q -- useful arithmetic,
-    not executed lanes.
+    the active-set iterations and the active-set size q (the mean final size
+    the kernels report, hmpc_solve_batch_stats) -- useful arithmetic, not
+    executed lanes.
 
     dense (condensed, NV = 6N): Hessian rows 210 N(N+1) + Cholesky NV^3/3 +
       unconstrained 2 NV^2 + per iteration (2 NV^2 + 4 q NV + q^2) + 400 N
@@ -234,7 +235,8 @@ def main():
                x=torch.empty((B, N + 1, 12), dtype=torch.float64, device=dev),
                obj=torch.empty(B, dtype=torch.float64, device=dev),
                status=torch.empty(B, dtype=torch.int32, device=dev),
-               iters=torch.empty(B, dtype=torch.int32, device=dev))
+               iters=torch.empty(B, dtype=torch.int32, device=dev),
+               active=torch.empty(B, dtype=torch.int32, device=dev))   # final active-set sizes
     stream = torch.cuda.current_stream(dev)
     # N > 1: the exchange step (per-instance cost + status) is one
     # all-gather of a packed [obj | status] slot on a side stream, pipelined
@@ -284,6 +286,7 @@ def main():
 
     st = last[0]['status'].cpu().numpy()
     it = out['iters'].cpu().numpy()
+    act = out['active'].cpu().numpy()
     solved_local = float((st == 0).mean())
     sf = torch.tensor([solved_local], dtype=torch.float64, device=dev)
     if world > 1:
@@ -307,7 +310,8 @@ def main():
         bpsolve = algorithmic_bytes(N)
         achieved = bpsolve * B / (kern_ms * 1e-3) / 1e9
         iters_mean = float(it.mean())
-        flops = algorithmic_flops(kernel, N, iters_mean, min(iters_mean, 6 * N))
+        q_mean = float(act.mean())   # the kernels' reported final active-set sizes
+        flops = algorithmic_flops(kernel, N, iters_mean, q_mean)
         traffic = executed = None
         wl = f'{args.variant}_N{N}_B{B}_{"straight" if args.straight else "curve"}' \
              f'{"_musweep" if args.mu_sweep else ""}' \
@@ -329,8 +333,10 @@ def main():
         f32 = 'float' in kernel
         vec_key = 'fp32_vector' if f32 else 'fp64_vector'
         p64, p32, peak_src = measured_peaks()
-        vec_peak = p32 if f32 else p64
+        vec_meas = p32 if f32 else p64
         vec_spec = FP32_VECTOR_SPEC_TFS if f32 else FP64_VECTOR_SPEC_TFS
+        vec_ach = flops * B / (kern_ms * 1e-3) / 1e12
+        prec = 'fp32' if f32 else 'fp64'
         rec = {
             'metric': METRIC,
             'value': total / el,
@@ -352,7 +358,8 @@ def main():
                        'precision': args.precision, 'parallelism': f'shard{world}'},
             'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS,
                          'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic,
-                         'limiter': 'not HBM: fp64 VALU issue (valu.busy) and dependent-chain latency of '
+                         'bound_effective': f'{prec}_valu_latency',
+                         'limiter': f'not HBM: {prec} VALU issue (valu.busy) and dependent-chain latency of '
                                     'an LDS/register-resident iterative solve (SURVEY 8d, DESIGN 5)',
                          'hbm_note': 'the HBM roofline is unreachable by design: a solve moves '
                                      f'{algorithmic_bytes(N)} B, so 40 % of 8 TB/s would need '
@@ -366,16 +373,20 @@ def main():
                                          'when no profile of this workload and kernel'},
             # the bound that matters for this path: fp64 VALU
             vec_key: {
-                'achieved': flops * B / (kern_ms * 1e-3) / 1e12, 'peak': vec_peak,
-                'peak_source': peak_src, 'peak_spec': vec_spec,
-                'unit': 'TFLOP/s', 'frac': flops * B / (kern_ms * 1e-3) / 1e12 / vec_peak,
-                'flops_per_solve': flops, 'basis': 'algorithmic (bench.algorithmic_flops, DESIGN.md 5)',
+                'achieved': vec_ach, 'peak': vec_spec, 'peak_source': 'datasheet (MI355X_MICROARCH.md)',
+                'unit': 'TFLOP/s', 'frac': vec_ach / vec_spec,
+                'peak_measured': vec_meas, 'peak_measured_source': peak_src,
+                'frac_measured': vec_ach / vec_meas,
+                'flops_per_solve': flops, 'basis': 'algorithmic (bench.algorithmic_flops, DESIGN.md 5) at the '
+                                                    'measured iters_mean and active_mean',
+                'iters_mean': iters_mean, 'active_mean': q_mean,
                 'executed_flops_per_solve': executed,
-                'executed_frac': (executed * B / (kern_ms * 1e-3) / 1e12 / vec_peak) if executed else None},
+                'executed_frac': (executed * B / (kern_ms * 1e-3) / 1e12 / vec_spec) if executed else None},
             'valu': valu,
             'cpu_baseline': base,
             'solved_frac_min_rank': float(sf[0]),
             'iters_mean': iters_mean, 'iters_max': int(it.max()),
+            'active_mean': q_mean, 'active_max': int(act.max()),
             'parity_sample': parity,
             'dist': dist_info,
         }

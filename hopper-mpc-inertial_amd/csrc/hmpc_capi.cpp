@@ -84,7 +84,7 @@ hmpc::SolveArgs make_args(hmpc_ctx* c, int64_t B, const double* x_in, const doub
                           int32_t* iters, int shift_mode) {
   hmpc::SolveArgs a;
   a.x_in = x_in; a.x_lin = x_lin; a.x_ref = x_ref; a.pf = pf; a.C = C; a.mu = mu;
-  a.u = u; a.x = x; a.obj = obj; a.status = status; a.iters = iters;
+  a.u = u; a.x = x; a.obj = obj; a.status = status; a.iters = iters; a.active = nullptr;
   a.B = B;
   a.dt = c->t; a.m = c->m; a.g = c->g; a.mu_default = c->mu;
   memcpy(a.Jinv, c->Jinv, sizeof(a.Jinv));
@@ -333,7 +333,7 @@ int check_solve_args(hmpc_ctx* c, int64_t B, const void* x_in, const void* x_lin
 
 extern "C" {
 
-int hmpc_version(void) { return 10200; }
+int hmpc_version(void) { return 10300; }
 
 int hmpc_supported_horizons(int variant, int* Ns, int cap) {
   return hmpc::supported_horizons(variant, Ns, cap);
@@ -446,17 +446,26 @@ int hmpc_set_precision(hmpc_ctx* c, int precision) {
   return HMPC_OK;
 }
 
-int hmpc_solve_batch(hmpc_ctx* c, int64_t B, const double* x_in, const double* x_lin,
-                     const double* x_ref, const double* pf, const double* C, const double* mu,
-                     double* u, double* x, double* obj, int32_t* status, int32_t* iters,
-                     void* stream) {
+int hmpc_solve_batch_stats(hmpc_ctx* c, int64_t B, const double* x_in, const double* x_lin,
+                           const double* x_ref, const double* pf, const double* C, const double* mu,
+                           double* u, double* x, double* obj, int32_t* status, int32_t* iters,
+                           int32_t* active, void* stream) {
   int rc = check_solve_args(c, B, x_in, x_lin, x_ref, pf, C, u, status);
   if (rc != HMPC_OK || B == 0) return rc;
   HMPC_HIP(c, hipSetDevice(c->device));
   hmpc::SolveArgs a = make_args(c, B, x_in, x_lin, x_ref, pf, C, mu, u, x, obj, status, iters, 0);
+  a.active = active;
   if ((rc = order_stream(c, (hipStream_t)stream)) != HMPC_OK) return rc;
   if ((rc = run_solve(c, a, (hipStream_t)stream)) != HMPC_OK) return rc;
   return mark_stream(c, (hipStream_t)stream);
+}
+
+int hmpc_solve_batch(hmpc_ctx* c, int64_t B, const double* x_in, const double* x_lin,
+                     const double* x_ref, const double* pf, const double* C, const double* mu,
+                     double* u, double* x, double* obj, int32_t* status, int32_t* iters,
+                     void* stream) {
+  return hmpc_solve_batch_stats(c, B, x_in, x_lin, x_ref, pf, C, mu, u, x, obj, status, iters, nullptr,
+                                stream);
 }
 
 int hmpc_time_solve_batch(hmpc_ctx* c, int64_t B, const double* x_in, const double* x_lin,

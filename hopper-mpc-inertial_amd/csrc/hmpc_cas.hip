@@ -491,6 +491,7 @@ __device__ void cas_solve(const SolveArgs& a, int N, int64_t b, double* sm, doub
     if (a.obj) a.obj[b] = objv;
     a.status[b] = status;
     if (a.iters) a.iters[b] = iters;
+      if (a.active) a.active[b] = qn;
   }
 }
 

@@ -20,6 +20,7 @@ struct SolveArgs {
   double* obj;           // [B] or nullptr
   int32_t* status;       // [B]
   int32_t* iters;        // [B] or nullptr
+  int32_t* active;       // [B] final active-set size, or nullptr
   int64_t B;
   double dt, m, g, mu_default;
   double Jinv[9];

@@ -1647,6 +1647,7 @@ __device__ __forceinline__ void solve_instance(const SolveArgs& a, int64_t b, re
       if (a.obj) a.obj[b] = objv;
       a.status[b] = status;
       if (a.iters) a.iters[b] = iters;
+      if (a.active) a.active[b] = q;
     }
   }
 }

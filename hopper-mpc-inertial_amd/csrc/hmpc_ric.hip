@@ -44,24 +44,10 @@ namespace hmpc {
 namespace {
 
 constexpr int RT = 64;   // one wavefront per workgroup
-// MRHS (speculative candidate columns): 0 off, 1 in the
-// one-wave-per-SIMD kernels (three-deep ring), 2 in every main-pass kernel
-#ifndef HMPC_RIC_MRHS
-#define HMPC_RIC_MRHS 2
-#endif
-#ifndef HMPC_RIC_MRL
-#define HMPC_RIC_MRL 1   // MRHS columns in LDS where they fit (A/B: 0)
-#endif
-#ifndef HMPC_RIC_UNIFY
-#define HMPC_RIC_UNIFY 1   // single-RHS sweeps through the MRHS body too (A/B: 0)
-#endif
-#ifndef HMPC_RIC_ZWIDE
-#define HMPC_RIC_ZWIDE 1   // the cached-column z with a lane's entries side by side: 1 one-wave kernels, 2 all, 0 off
-#endif
-#ifndef HMPC_RIC_NSC
-#define HMPC_RIC_NSC 16
-#endif
-constexpr int kNSC = HMPC_RIC_MRHS ? HMPC_RIC_NSC : 0;   // candidate cache slots per workgroup (<= 64)
+// MRHS (speculative candidate columns) in every main-pass
+// kernel, their four columns in LDS, the single-RHS sweeps through the same
+// body; 16 candidate cache slots per workgroup (<= 64; 32 measured no better)
+constexpr int kNSC = 16;
 constexpr int kMRK = 4;                         // right-hand sides per sweep pair (DPP rows)
 
 // LDS layout (in doubles) for a runtime horizon N and active-set capacity cap
@@ -171,10 +157,7 @@ __device__ __forceinline__ void vset(double (&v)[ENT], int i, double x) {
   for (int e = 0; e < ENT; ++e) v[e] = (64 * e + lane == i) ? x : v[e];
 }
 
-#ifndef HMPC_RIC_ZCREL
-#define HMPC_RIC_ZCREL 1e-3
-#endif
-constexpr double kZcRel = HMPC_RIC_ZCREL;
+constexpr double kZcRel = 1e-3;   // the z-fallback threshold
 // ZC: z = H^-1 (n_p - N_A r) as s - sum_a r_a S_a from the cached columns
 // S_a = H^-1 n_a of the active rows (scw: cap x NV, kept in active order),
 // instead of a third pair of sweeps per iteration
@@ -216,10 +199,10 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
   double* cbv = sm + L.CB;
   double* sdg = sm + L.SD;
   double* un = sm + L.U0;
-  constexpr bool kMR = ENT == 1 && ZC && (HMPC_RIC_MRHS >= 2 || (HMPC_RIC_MRHS == 1 && RING != 2));
+  constexpr bool kMR = ENT == 1 && ZC;
   // ... with its four columns in LDS (SV, ZV, MU and the union's 568-double
   // Riccati scratch, all dead during the s sweep pair; 6N <= 568 for N <= 64)
-  constexpr bool kMRL = kMR && HMPC_RIC_MRL;
+  constexpr bool kMRL = kMR;
   static_assert(6 * kRicNmax <= 568, "an MRHS column must fit the union's Riccati scratch");
   // MRHS candidate columns: after the cached active columns S (cap x NV)
   [[maybe_unused]] double* gcache = kMR ? scw + (int64_t)cap * NV : nullptr;
@@ -548,17 +531,9 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
   // DPP inside asm, so the block covers the worst hazard in front of it
   // itself -- an SALU write of EXEC (the lane < 6 stores) followed by a DPP
   // op needs 5 wait states (a VALU write of x, 2).
-#ifndef HMPC_OVF_DPP
-#define HMPC_OVF_DPP 0   // 1: the DPP blocks in the overflow pass too (A/B)
-#endif
-#ifndef HMPC_DPP_TAIL
-#define HMPC_DPP_TAIL ""   // A/B: "s_nop 4" after every block
-#endif
-#ifndef HMPC_DPP_BC
-#define HMPC_DPP_BC ""     // A/B: " bound_ctrl:1" (a disabled source lane reads 0)
-#endif
-#define HMPC_DPPF(acc, x, k, n) "v_fmac_f64_dpp %" #acc ", %" #x ", %" #k " row_newbcast:" #n " row_mask:0xf bank_mask:0xf" HMPC_DPP_BC "\n\t"
-#define HMPC_DPPFN(acc, x, k, n) "v_fmac_f64_dpp %" #acc ", %" #x ", -%" #k " row_newbcast:" #n " row_mask:0xf bank_mask:0xf" HMPC_DPP_BC "\n\t"
+// The overflow pass (ENT > 1) keeps the readlane form.
+#define HMPC_DPPF(acc, x, k, n) "v_fmac_f64_dpp %" #acc ", %" #x ", %" #k " row_newbcast:" #n " row_mask:0xf bank_mask:0xf\n\t"
+#define HMPC_DPPFN(acc, x, k, n) "v_fmac_f64_dpp %" #acc ", %" #x ", -%" #k " row_newbcast:" #n " row_mask:0xf bank_mask:0xf\n\t"
   struct BwdL {
     double cp, sp, st, b0, b1, b2, n, kc[6];
   };
@@ -653,10 +628,10 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
         }
         // B_j'lam over lam[6..11] (lanes 6..11 of li)
         double bc;
-        if constexpr (ENT == 1 || HMPC_OVF_DPP) {
+        if constexpr (ENT == 1) {
           double bc0 = 0.0, bc1 = 0.0;
           asm("s_nop 4\n\t" HMPC_DPPF(0, 2, 3, 6) HMPC_DPPF(1, 2, 4, 7) HMPC_DPPF(0, 2, 5, 8)
-              HMPC_DPPF(1, 2, 6, 9) HMPC_DPPF(0, 2, 7, 10) HMPC_DPPF(1, 2, 8, 11) HMPC_DPP_TAIL
+              HMPC_DPPF(1, 2, 6, 9) HMPC_DPPF(0, 2, 7, 10) HMPC_DPPF(1, 2, 8, 11)
               : "+v"(bc0), "+v"(bc1)
               : "v"(li), "v"(k6), "v"(k7), "v"(k8), "v"(d.b0), "v"(d.b1), "v"(d.b2));
           bc = bc0 + bc1;
@@ -677,9 +652,9 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
         const double s6 = row_shift<-6>(li), s5 = row_shift<-5>(li), s7 = row_shift<-7>(li);
         double a0 = fma(fma(gB, d.cp, gA), s6, li), a1 = (gC * d.sp) * s5, a2 = (gD * d.sp) * s7;
         // + K_j[:, i]'mu_j, mu_j in lanes 0..5 of m
-        if constexpr (ENT == 1 || HMPC_OVF_DPP) {
+        if constexpr (ENT == 1) {
           asm("s_nop 4\n\t" HMPC_DPPF(0, 3, 4, 0) HMPC_DPPF(1, 3, 5, 1) HMPC_DPPF(2, 3, 6, 2)
-              HMPC_DPPF(0, 3, 7, 3) HMPC_DPPF(1, 3, 8, 4) HMPC_DPPF(2, 3, 9, 5) HMPC_DPP_TAIL
+              HMPC_DPPF(0, 3, 7, 3) HMPC_DPPF(1, 3, 8, 4) HMPC_DPPF(2, 3, 9, 5)
               : "+v"(a0), "+v"(a1), "+v"(a2)
               : "v"(m), "v"(d.kc[0]), "v"(d.kc[1]), "v"(d.kc[2]), "v"(d.kc[3]), "v"(d.kc[4]), "v"(d.kc[5]));
         } else {
@@ -694,24 +669,8 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
       };
       // (loads are unconditional -- out-of-range steps reload stage 0 -- so
       // that the vmcnt/lgkmcnt waits stay counted, not drained)
-      if constexpr (RING >= 4) {   // RING-deep (1 wave/SIMD: K loads that miss L2)
-        BwdL R[RING];
-#pragma unroll
-        for (int p = 0; p < RING - 1; ++p) load_b(jt >= p ? jt - p : 0, R[p]);
-        for (int j = jt; j >= 0; j -= RING) {
-          bool go = true;
-#pragma unroll
-          for (int i = 0; i < RING; ++i) {
-            if (go) {
-              const int jj = j - i, jl = jj - (RING - 1);
-              load_b(jl >= 0 ? jl : 0, R[(i + RING - 1) % RING]);
-              bstep(jj, R[i]);
-              if (jj < 1) go = false;
-            }
-          }
-          if (!go) break;
-        }
-      } else if constexpr (RING == 3) {
+      static_assert(RING == 2 || RING == 3, "ring depth");
+      if constexpr (RING == 3) {
         BwdL R0, R1, R2;
         load_b(jt, R0);
         load_b(jt >= 1 ? jt - 1 : 0, R1);
@@ -780,11 +739,11 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
       auto fstep = [&](int k, const FwdL& d) __attribute__((always_inline)) {
         // u = w - K_k x (x in lanes 0..11 of xi)
         double a0 = d.w, a1 = 0.0;
-        if constexpr (ENT == 1 || HMPC_OVF_DPP) {
+        if constexpr (ENT == 1) {
           asm("s_nop 4\n\t" HMPC_DPPFN(0, 2, 3, 0) HMPC_DPPFN(1, 2, 4, 1) HMPC_DPPFN(0, 2, 5, 2)
               HMPC_DPPFN(1, 2, 6, 3) HMPC_DPPFN(0, 2, 7, 4) HMPC_DPPFN(1, 2, 8, 5)
               HMPC_DPPFN(0, 2, 9, 6) HMPC_DPPFN(1, 2, 10, 7) HMPC_DPPFN(0, 2, 11, 8)
-              HMPC_DPPFN(1, 2, 12, 9) HMPC_DPPFN(0, 2, 13, 10) HMPC_DPPFN(1, 2, 14, 11) HMPC_DPP_TAIL
+              HMPC_DPPFN(1, 2, 12, 9) HMPC_DPPFN(0, 2, 13, 10) HMPC_DPPFN(1, 2, 14, 11)
               : "+v"(a0), "+v"(a1)
               : "v"(xi), "v"(d.kr[0]), "v"(d.kr[1]), "v"(d.kr[2]), "v"(d.kr[3]), "v"(d.kr[4]), "v"(d.kr[5]),
                 "v"(d.kr[6]), "v"(d.kr[7]), "v"(d.kr[8]), "v"(d.kr[9]), "v"(d.kr[10]), "v"(d.kr[11]));
@@ -819,9 +778,9 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
         const double r3 = m911 * d.br[3], r4 = m911 * d.br[4], r5 = m911 * d.br[5];
         double b0 = fma(fma(fB, d.cp, fA), s6, xi), b1 = (fC * d.sp) * s7, b2 = (fD * d.sp) * s5;
         // + B_k u_k, u_k in lanes 0..5 of u
-        if constexpr (ENT == 1 || HMPC_OVF_DPP) {
+        if constexpr (ENT == 1) {
           asm("s_nop 4\n\t" HMPC_DPPF(0, 3, 4, 0) HMPC_DPPF(1, 3, 5, 1) HMPC_DPPF(2, 3, 6, 2)
-              HMPC_DPPF(0, 3, 7, 3) HMPC_DPPF(1, 3, 8, 4) HMPC_DPPF(2, 3, 9, 5) HMPC_DPP_TAIL
+              HMPC_DPPF(0, 3, 7, 3) HMPC_DPPF(1, 3, 8, 4) HMPC_DPPF(2, 3, 9, 5)
               : "+v"(b0), "+v"(b1), "+v"(b2)
               : "v"(u), "v"(r0), "v"(r1), "v"(r2), "v"(r3), "v"(r4), "v"(r5));
         } else {
@@ -834,24 +793,7 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
         }
         xi = lr < 12 ? (b0 + b1) + b2 : 0.0;
       };
-      if constexpr (RING >= 4) {
-        FwdL R[RING];
-#pragma unroll
-        for (int p = 0; p < RING - 1; ++p) load_f(p < N ? p : N - 1, R[p]);
-        for (int k = 0; k < N; k += RING) {
-          bool go = true;
-#pragma unroll
-          for (int i = 0; i < RING; ++i) {
-            if (go) {
-              const int kk = k + i, kl = kk + RING - 1;
-              load_f(kl < N ? kl : N - 1, R[(i + RING - 1) % RING]);
-              fstep(kk, R[i]);
-              if (kk + 1 >= N) go = false;
-            }
-          }
-          if (!go) break;
-        }
-      } else if constexpr (RING == 3) {
+      if constexpr (RING == 3) {
         FwdL R0, R1, R2;
         load_f(0, R0);
         load_f(N >= 2 ? 1 : 0, R1);
@@ -881,7 +823,7 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
     else wsync();
   };
   auto hinv = [&](double* dst, int jt) __attribute__((always_inline)) {
-    if constexpr (ENT == 1 && ZC && HMPC_RIC_MRHS && HMPC_RIC_MRL && HMPC_RIC_UNIFY) {
+    if constexpr (ENT == 1 && ZC) {
       // one sweep body in the kernel: the MRHS form with a single row, its
       // column the destination (NB copied in first; dst is SV, ZV or VV)
       for (int i = lane; i < NV; i += RT) dst[i] = nb[i];
@@ -1194,7 +1136,7 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
         }
         rsync();
         bool sweep = !ZC;
-        if constexpr (ZC && (HMPC_RIC_ZWIDE >= 2 || (HMPC_RIC_ZWIDE == 1 && RING != 2))) {
+        if constexpr (ZC && RING != 2) {   // the one-wave kernels
           // z = s - S r streamed column by column, each lane's ZE entries
           // i = i0 + lane + 64 e side by side: 4 x ZE independent loads in flight
           // per lane per batch of 4 columns (the latency of the L2/MALL-resident
@@ -1446,6 +1388,7 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
       if (a.obj) a.obj[b] = objv;
       a.status[b] = status;
       if (a.iters) a.iters[b] = iters;
+      if (a.active) a.active[b] = q;
     }
   }
 }
@@ -1456,15 +1399,9 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
 // OCC = waves per SIMD the register allocation is held to (2: <= 256 VGPRs +
 // AGPRs; 1: up to 512)
 // sweep prefetch depth (ring slots) at 1 wave/SIMD
-#ifndef HMPC_RIC_RING1
-#define HMPC_RIC_RING1 3
-#endif
-constexpr int kRing1Wave = HMPC_RIC_RING1;
+constexpr int kRing1Wave = 3;   // (4-6 slots measured slower)
 // ... and at 2 waves/SIMD (register budget 256)
-#ifndef HMPC_RIC_RING2
-#define HMPC_RIC_RING2 2
-#endif
-constexpr int kRing2Wave = HMPC_RIC_RING2;
+constexpr int kRing2Wave = 2;
 template <int VAR, int OCC, int NC = 0, int CAPC = 0>
 __global__ void __launch_bounds__(RT) __attribute__((amdgpu_waves_per_eu(OCC, OCC))) ric_kernel(SolveArgs a, int N, int cap) {
   extern __shared__ __attribute__((aligned(16))) double ric_sm[];
@@ -1543,13 +1480,10 @@ RicCfg ric_config(int N) {
 
 int ric_qcap(int N) { return ric_config(N).cap; }
 int ric_occ(int N) { return ric_config(N).occ; }
-#ifndef HMPC_RIC_STATIC20
-#define HMPC_RIC_STATIC20 1   // 0: configs[3]'s N = 20 on the runtime-N kernel (A/B)
-#endif
 int ric_static_n(int N) {
   const RicCfg c = ric_config(N);
   if (N == 60 && c.occ == 1 && c.cap == 47) return 60;
-  if (HMPC_RIC_STATIC20 && N == 20 && c.occ == 2 && c.cap == 38) return 20;
+  if (N == 20 && c.occ == 2 && c.cap == 38) return 20;
   return 0;
 }
 

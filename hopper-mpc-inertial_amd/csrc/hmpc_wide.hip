@@ -749,6 +749,7 @@ __device__ void wide_solve(const SolveArgs& a, const int N, const int64_t b, T* 
       if (a.obj) a.obj[b] = objv;
       a.status[b] = status;
       if (a.iters) a.iters[b] = iters;
+      if (a.active) a.active[b] = q;
     }
   }
 }

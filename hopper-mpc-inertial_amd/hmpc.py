@@ -35,6 +35,7 @@ SIGNATURES = {
                                    ctypes.c_int, ctypes.c_int]),
     'hmpc_destroy': (ctypes.c_int, [_VP]),
     'hmpc_solve_batch': (ctypes.c_int, [_VP, ctypes.c_int64] + [_VP] * 11 + [_VP]),
+    'hmpc_solve_batch_stats': (ctypes.c_int, [_VP, ctypes.c_int64] + [_VP] * 12 + [_VP]),
     'hmpc_solve_batch_host': (ctypes.c_int, [_VP, ctypes.c_int64] + [_VP] * 11),
     'hmpc_mpcontrol_batch': (ctypes.c_int, [_VP, ctypes.c_int64, ctypes.c_int] + [_VP] * 10 + [_VP]),
     'hmpc_mpcontrol_plan_batch': (ctypes.c_int, [_VP, ctypes.c_int64, ctypes.c_int, _VP, _VP, _VP,
@@ -128,6 +129,7 @@ def _check_out(out, B, N, device, need_x=False):
     _check_tensor(out.get('obj'), (B,), "out['obj']", device, optional=True)
     _check_tensor(out.get('status'), (B,), "out['status']", device, dtype='int32')
     _check_tensor(out.get('iters'), (B,), "out['iters']", device, dtype='int32', optional=True)
+    _check_tensor(out.get('active'), (B,), "out['active']", device, dtype='int32', optional=True)
 
 
 class Context:
@@ -219,11 +221,13 @@ class Context:
                        iters=torch.empty(B, dtype=torch.int32, device=dev))
         _check_out(out, B, N, self.device)
         s = stream if stream is not None else torch.cuda.current_stream(x_in.device).cuda_stream
-        rc = self._lib.hmpc_solve_batch(self._h, B, _ptr(x_in), _ptr(x_lin), _ptr(x_ref), _ptr(pf),
-                                        _ptr(C), _ptr(mu), _ptr(out['u']), _ptr(out.get('x')),
-                                        _ptr(out.get('obj')), _ptr(out['status']),
-                                        _ptr(out.get('iters')), ctypes.c_void_p(s))
-        self._check(rc, 'hmpc_solve_batch')
+        # out['active'] (optional, int32 [B]): each instance's final active-set size
+        rc = self._lib.hmpc_solve_batch_stats(self._h, B, _ptr(x_in), _ptr(x_lin), _ptr(x_ref), _ptr(pf),
+                                              _ptr(C), _ptr(mu), _ptr(out['u']), _ptr(out.get('x')),
+                                              _ptr(out.get('obj')), _ptr(out['status']),
+                                              _ptr(out.get('iters')), _ptr(out.get('active')),
+                                              ctypes.c_void_p(s))
+        self._check(rc, 'hmpc_solve_batch_stats')
         return out
 
     def mpcontrol_device(self, init, x_in, x_ref, pf, C, x_prev, mu=None, out=None, stream=None):

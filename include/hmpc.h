@@ -91,7 +91,8 @@ typedef struct hmpc_ctx hmpc_ctx;
 
 /* ABI version (major*10000 + minor*100 + patch): 1.2.0 = 1.0 + the fp32 dense
    build, HMPC_PREC_F64_RICCATI / _F64_DENSE / _F32_GENERIC, hmpc_kernel_name,
-   hmpc_active_capacity, hmpc_plan_batch, hmpc_gait_batch, HMPC_VARIANT_CAS */
+   hmpc_active_capacity, hmpc_plan_batch, hmpc_gait_batch, HMPC_VARIANT_CAS;
+   1.3.0 = + hmpc_solve_batch_stats */
 int hmpc_version(void);
 
 /* Which horizons have a dedicated (one- or two-wavefront) kernel for
@@ -141,6 +142,16 @@ int hmpc_solve_batch(hmpc_ctx* ctx, int64_t B,
                      const double* pf, const double* C, const double* mu,
                      double* u, double* x, double* obj, int32_t* status, int32_t* iters,
                      void* stream);
+
+/* hmpc_solve_batch plus one more output: active [B] receives each
+   instance's final active-set size (the number of inequality rows active at
+   the optimum the solver certifies; may be NULL).  The bench feeds its mean
+   into the algorithmic flop count (bench.algorithmic_flops). */
+int hmpc_solve_batch_stats(hmpc_ctx* ctx, int64_t B,
+                           const double* x_in, const double* x_lin, const double* x_ref,
+                           const double* pf, const double* C, const double* mu,
+                           double* u, double* x, double* obj, int32_t* status, int32_t* iters,
+                           int32_t* active, void* stream);
 
 /* Same with host pointers; synchronous. */
 int hmpc_solve_batch_host(hmpc_ctx* ctx, int64_t B,

@@ -34,7 +34,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_version_and_horizons():
     lib = hmpc.load()
-    assert lib.hmpc_version() == 10200   # 1.2: planner, CasADi variant, precisions 4-5, capacity
+    assert lib.hmpc_version() == 10300   # 1.3: + hmpc_solve_batch_stats (1.2: planner, CasADi, precisions 4-5, capacity)
     hs = hmpc.supported_horizons('3f')
     assert 10 in hs and 20 in hs
     assert hmpc.supported_horizons('2f') == hs

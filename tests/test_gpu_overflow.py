@@ -12,6 +12,8 @@ counted on the CPU from the port's solution against the reference-form
 constraint rows (oracle/hmpc_oracle.build_qp), so the test proves the cases
 really exceed the capacities it claims to cover.
 """
+import os
+
 import numpy as np
 import pytest
 from conftest import DENSE10_3F
@@ -85,7 +87,8 @@ def test_overflow_n10(hm, precision, kernel):
     N, B = 10, 48
     inst = adversarial(B, N, 2, 50.0, 8.0, mu=0.2)   # optimal active sets up to 55 of 60
     gpu, ref, k, cap = solve_both(hm, N, inst, precision)
-    assert k == kernel
+    if 'HMPC_LIB' not in os.environ:   # (an A/B build may dispatch other classes)
+        assert k == kernel
     assert (ref['status'] == 0).all()
     assert np.array_equal(gpu['status'], ref['status'])
     assert np.abs(gpu['u'] - ref['u']).max() <= U_TOL
