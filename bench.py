@@ -85,6 +85,9 @@ def workload_label(args, world):
     curve = not args.straight
     if args.precision in ('f32', 'f32_generic') and args.variant == '3f' and args.N == 10:
         return f'configs[4]: batch={gb}, 3f, N=10, fp32 (vs fp64) tolerance/throughput trade-off'
+    if args.precision == 'f32_refined' and args.variant == '3f' and args.N == 10:
+        return (f'configs[4]: batch={gb}, 3f, N=10, fp32 + {args.refine} fp64 corrections (vs fp64) '
+                f'tolerance/throughput trade-off')
     if args.variant == '2f' and args.N == 10 and not curve:
         return f'configs[1]: batch={gb} randomised x0, 2f (planar, Fy=0), horizon N=10, fp64'
     if args.variant == '3f' and args.N == 10 and curve:
@@ -113,9 +116,12 @@ def parse():
     ap.add_argument('--mu-sweep', action='store_true', help='mu ~ U(0.3, 1.2)')
     ap.add_argument('--seed', type=int, default=2024)
     ap.add_argument('--precision', default='f64',
-                    choices=['f64', 'f32', 'f64_generic', 'f64_riccati', 'f64_dense', 'f32_generic'],
+                    choices=['f64', 'f32', 'f32_refined', 'f64_generic', 'f64_riccati', 'f64_dense',
+                             'f32_generic'],
                     help='f64 = the fastest fp64 kernel for N (default); f32 = fp32 one-wave '
-                         'kernel (configs[4]); others force a kernel for A/B runs')
+                         'kernel, f32_refined = fp32 + --refine fp64 corrections (configs[4]); '
+                         'others force a kernel for A/B runs')
+    ap.add_argument('--refine', type=int, default=2, help='fp64 corrections of f32_refined')
     ap.add_argument('--cpu-seconds', type=float, default=12.0,
                     help='budget of the bounded CPU-baseline sample, split over its two legs '
                          '(all cores, then one core); 0 disables')
@@ -230,6 +236,8 @@ def main():
     c = hmpc_plan.runner_constants()
     ctx = hmpc.Context(args.variant, N, t=c['t'], m=c['m'], g=c['g'], mu=1.0, Jinv=c['Jinv'],
                        rh=c['rh'], device=local, precision=args.precision)
+    if args.precision == 'f32_refined':
+        ctx.set_refinement(args.refine)
     kernel = ctx.kernel_name
     out = dict(u=torch.empty((B, N, 6), dtype=torch.float64, device=dev),
                x=torch.empty((B, N + 1, 12), dtype=torch.float64, device=dev),
@@ -348,7 +356,8 @@ def main():
             'higher_is_better': True,
             'scaling': 'strong' if args.global_batch else 'weak',
             'vs_baseline': None,
-            'dtype': 'f32' if args.precision in ('f32', 'f32_generic') else 'f64',
+            'dtype': {'f32': 'f32', 'f32_generic': 'f32', 'f32_refined': 'f32+f64 refinement'}.get(args.precision,
+                                                                                                   'f64'),
             'data': 'synthetic: Runner path_plan_init plan + randomised x0 (SURVEY.md 8d), generated on '
                     'host, resident in HBM before timing',
             'config': {'workload': workload_label(args, world), 'global_batch': B * world

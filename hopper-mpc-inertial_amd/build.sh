@@ -34,7 +34,7 @@ cmp_flags() {
 # body (hundreds of s_movs) out of that loop and hold them for the kernel's
 # life: SGPR spills into VGPR lanes, then scratch (556 B/lane in the
 # compacted class; 40 B without it).  Off for the split horizons' objects.
-SPLIT_FLAGS=${SPLIT_FLAGS-"-mllvm -disable-machine-licm"}
+SPLIT_FLAGS=${SPLIT_FLAGS-""}   # "-mllvm -disable-machine-licm" with -DHMPC_SPLIT_PERSIST=1
 CMPOBJS=""
 for n in $HORIZONS; do
   $HIPCC $FLAGS -DHMPC_INST_N=$n $(cmp_flags $n) $([ -n "$(cmp_flags $n)" ] && echo $SPLIT_FLAGS) -c ${KSRC:-csrc/hmpc_kernels.hip} -o $BDIR/hmpc_kernels_n$n.o "$@" &
@@ -51,8 +51,12 @@ for n in $F32_HORIZONS; do
   $HIPCC $FLAGS -DHMPC_INST_N=$n -DHMPC_REAL=float -DHMPC_LAUNCH_SUFFIX=_f32 "-DHMPC_WAVES_PER_EU(W)=$F32_WAVES" \
     -c csrc/hmpc_kernels.hip -o $BDIR/hmpc_kernels_n${n}_f32.o "$@" &
   pids+=($!)
+  # fp32 + fp64 refinement (HMPC_PREC_F32_REFINED)
+  $HIPCC $FLAGS -DHMPC_INST_N=$n -DHMPC_REAL=float -DHMPC_F32_REFINE=1 -DHMPC_LAUNCH_SUFFIX=_f32r \
+    "-DHMPC_WAVES_PER_EU(W)=$F32_WAVES" -c csrc/hmpc_kernels.hip -o $BDIR/hmpc_kernels_n${n}_f32r.o "$@" &
+  pids+=($!)
 done
-$HIPCC $FLAGS "-DHMPC_HORIZON_LIST(X)=$LIST" "-DHMPC_F32_LIST(X)=$F32LIST" -c csrc/hmpc_dispatch.cpp -o $BDIR/hmpc_dispatch.o &
+$HIPCC $FLAGS "-DHMPC_HORIZON_LIST(X)=$LIST" "-DHMPC_F32_LIST(X)=$F32LIST" "-DHMPC_F32R_LIST(X)=$F32LIST" -c csrc/hmpc_dispatch.cpp -o $BDIR/hmpc_dispatch.o &
 pids+=($!)
 $HIPCC $FLAGS -c csrc/hmpc_capi.cpp -o $BDIR/hmpc_capi.o &
 pids+=($!)
@@ -70,7 +74,7 @@ for p in "${pids[@]}"; do wait "$p"; done
 objs=""
 for n in $HORIZONS; do objs="$objs $BDIR/hmpc_kernels_n$n.o"; done
 objs="$objs $CMPOBJS"
-for n in $F32_HORIZONS; do objs="$objs $BDIR/hmpc_kernels_n${n}_f32.o"; done
+for n in $F32_HORIZONS; do objs="$objs $BDIR/hmpc_kernels_n${n}_f32.o $BDIR/hmpc_kernels_n${n}_f32r.o"; done
 # every object but the ABI/dispatch host code, for tests/test_sanitizers.py (which
 # rebuilds those two under ASan/UBSan and links the kernels as built)
 echo $objs $BDIR/hmpc_plant.o $BDIR/hmpc_planner.o $BDIR/hmpc_cas.o $BDIR/hmpc_wide.o $BDIR/hmpc_ric.o | tr ' ' '\n' > $BDIR/objs.txt

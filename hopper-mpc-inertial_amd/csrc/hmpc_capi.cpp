@@ -25,6 +25,7 @@ struct hmpc_ctx {
   double rh[3];
   int uref_mode;
   int precision = HMPC_PREC_F64;
+  int refine = 2;   // fp64 corrections of HMPC_PREC_F32_REFINED (hmpc_set_refinement)
   std::string err;
   // staging buffers (host API) and mpcontrol scratch
   void* dbuf = nullptr;
@@ -103,6 +104,7 @@ hmpc::SolveArgs make_args(hmpc_ctx* c, int64_t B, const double* x_in, const doub
   a.split_fork = nullptr;
   a.split_join[0] = a.split_join[1] = nullptr;
   a.precision = c->precision;
+  a.refine = c->refine;
   return a;
 }
 
@@ -171,7 +173,8 @@ int prepare_ric(hmpc_ctx* c, int64_t B, hmpc::SolveArgs& a) {
     return HMPC_OK;
   }
   // (the fp32 dense build hands its overflows to the same fp64 pass)
-  if ((k != hmpc::Kernel::Dense && k != hmpc::Kernel::DenseF32 && k != hmpc::Kernel::Riccati) ||
+  if ((k != hmpc::Kernel::Dense && k != hmpc::Kernel::DenseF32 && k != hmpc::Kernel::DenseF32R &&
+       k != hmpc::Kernel::Riccati) ||
       c->N > hmpc::kRicNmax)
     return HMPC_OK;
   const int64_t rstride = hmpc::ric_rws_stride(c->N);
@@ -194,7 +197,7 @@ int prepare_ric(hmpc_ctx* c, int64_t B, hmpc::SolveArgs& a) {
   // the dense kernel's split launch (narrower kernels for the instances with
   // few free variables): class counts and claim counters next to the
   // overflow counters, which the overflow pass zeroes together at its end
-  if (k == hmpc::Kernel::Dense && hmpc::dense_split_nv(c->N, false) > 0) {
+  if (k == hmpc::Kernel::Dense && hmpc::dense_split_nv(c->N, 0) > 0) {
     if (B > c->split_cap) {
       if (c->split) (void)hipFree(c->split);
       c->split = nullptr;
@@ -205,7 +208,15 @@ int prepare_ric(hmpc_ctx* c, int64_t B, hmpc::SolveArgs& a) {
     }
     if (!c->split_fork) {
       int least = 0, greatest = 0;
-      if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess ||
+#ifndef HMPC_SPLIT_PRIO
+#define HMPC_SPLIT_PRIO 0
+#endif
+      if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) {
+        c->err = "stream priority range";
+        return HMPC_ERR_HIP;
+      }
+      if (!HMPC_SPLIT_PRIO) least = greatest = 0;
+      if (
           hipStreamCreateWithPriority(&c->split_stream[0], hipStreamNonBlocking, greatest) != hipSuccess ||
           hipStreamCreateWithPriority(&c->split_stream[1], hipStreamNonBlocking, least) != hipSuccess ||
           hipEventCreateWithFlags(&c->split_join[0], hipEventDisableTiming) != hipSuccess ||
@@ -388,9 +399,11 @@ int hmpc_active_capacity(hmpc_ctx* c) {
   if (!c) return -1;
   switch (hmpc::pick_kernel(c->variant, c->N, c->precision)) {
     case hmpc::Kernel::Dense:
-      return hmpc::dense_qmax(c->N, false);
+      return hmpc::dense_qmax(c->N, 0);
     case hmpc::Kernel::DenseF32:
-      return hmpc::dense_qmax(c->N, true);
+      return hmpc::dense_qmax(c->N, 1);
+    case hmpc::Kernel::DenseF32R:
+      return hmpc::dense_qmax(c->N, 2);
     case hmpc::Kernel::Riccati:
       return hmpc::ric_qcap(c->N);
     case hmpc::Kernel::Cas:
@@ -407,9 +420,11 @@ const char* hmpc_kernel_name(hmpc_ctx* c) {
   const bool v3 = c->variant == HMPC_VARIANT_3F;
   switch (hmpc::pick_kernel(c->variant, c->N, c->precision)) {
     case hmpc::Kernel::Dense:
-      return hmpc::dense_name(c->variant, c->N, false);
+      return hmpc::dense_name(c->variant, c->N, 0);
     case hmpc::Kernel::DenseF32:
-      return hmpc::dense_name(c->variant, c->N, true);
+      return hmpc::dense_name(c->variant, c->N, 1);
+    case hmpc::Kernel::DenseF32R:
+      return hmpc::dense_name(c->variant, c->N, 2);
     case hmpc::Kernel::Cas:
       return "hmpc::cas_kernel";
     case hmpc::Kernel::Riccati:
@@ -434,7 +449,7 @@ int hmpc_set_precision(hmpc_ctx* c, int precision) {
   if (!c) return HMPC_ERR_ARG;
   if (precision != HMPC_PREC_F64 && precision != HMPC_PREC_F32 && precision != HMPC_PREC_F64_GENERIC &&
       precision != HMPC_PREC_F64_RICCATI && precision != HMPC_PREC_F64_DENSE &&
-      precision != HMPC_PREC_F32_GENERIC) {
+      precision != HMPC_PREC_F32_GENERIC && precision != HMPC_PREC_F32_REFINED) {
     c->err = "unknown precision";
     return HMPC_ERR_ARG;
   }
@@ -443,6 +458,16 @@ int hmpc_set_precision(hmpc_ctx* c, int precision) {
     return HMPC_ERR_UNSUPPORTED;
   }
   c->precision = precision;
+  return HMPC_OK;
+}
+
+int hmpc_set_refinement(hmpc_ctx* c, int corrections) {
+  if (!c) return HMPC_ERR_ARG;
+  if (corrections < 0 || corrections > 16) {
+    c->err = "corrections outside [0, 16]";
+    return HMPC_ERR_ARG;
+  }
+  c->refine = corrections;
   return HMPC_OK;
 }
 

@@ -9,9 +9,13 @@
 #ifndef HMPC_HORIZON_LIST
 #define HMPC_HORIZON_LIST(X) X(5) X(10) X(20)
 #endif
-// horizons with an fp32 build of the dense kernel (launch_solve_n<N>_f32)
+// horizons with an fp32 build of the dense kernel (launch_solve_n<N>_f32) and
+// with an fp32 + fp64-refinement build (launch_solve_n<N>_f32r)
 #ifndef HMPC_F32_LIST
 #define HMPC_F32_LIST(X) X(10)
+#endif
+#ifndef HMPC_F32R_LIST
+#define HMPC_F32R_LIST(X) X(10)
 #endif
 
 namespace hmpc {
@@ -30,12 +34,27 @@ HMPC_HORIZON_LIST(HMPC_DECL)
   const char* name_solve_n##n##_f32(int variant);
 HMPC_F32_LIST(HMPC_DECL)
 #undef HMPC_DECL
+#define HMPC_DECL(n)                                                            \
+  bool launch_solve_n##n##_f32r(int variant, const SolveArgs& a, hipStream_t s); \
+  int qmax_solve_n##n##_f32r();                                                  \
+  int split_nv_n##n##_f32r();                                                    \
+  const char* name_solve_n##n##_f32r(int variant);
+HMPC_F32R_LIST(HMPC_DECL)
+#undef HMPC_DECL
 
 static bool f32_compiled(int variant, int N) {
   if (variant != 2 && variant != 3) return false;
 #define HMPC_CASE(n) \
   if (N == n) return true;
   HMPC_F32_LIST(HMPC_CASE)
+#undef HMPC_CASE
+  return false;
+}
+static bool f32r_compiled(int variant, int N) {
+  if (variant != 2 && variant != 3) return false;
+#define HMPC_CASE(n) \
+  if (N == n) return true;
+  HMPC_F32R_LIST(HMPC_CASE)
 #undef HMPC_CASE
   return false;
 }
@@ -61,6 +80,8 @@ Kernel pick_kernel(int variant, int N, int precision) {
       return N <= kWideNmax ? Kernel::Wide : Kernel::None;
     case 3:
       return N <= kRicNmax ? Kernel::Riccati : Kernel::None;
+    case 6:
+      return f32r_compiled(variant, N) ? Kernel::DenseF32R : Kernel::None;
     case 4:
       return horizon_compiled(variant, N) ? Kernel::Dense : Kernel::None;
     case 0:
@@ -89,6 +110,12 @@ bool launch_solve(int variant, int N, const SolveArgs& a, hipStream_t s) {
       HMPC_F32_LIST(HMPC_CASE)
 #undef HMPC_CASE
       return false;
+    case Kernel::DenseF32R:
+#define HMPC_CASE(n) \
+  if (N == n) return launch_solve_n##n##_f32r(variant, a, s);
+      HMPC_F32R_LIST(HMPC_CASE)
+#undef HMPC_CASE
+      return false;
     case Kernel::Riccati:
       return launch_solve_ric(variant, N, a, s);
     case Kernel::Wide:
@@ -100,8 +127,15 @@ bool launch_solve(int variant, int N, const SolveArgs& a, hipStream_t s) {
   }
 }
 
-int dense_qmax(int N, bool f32) {
-  if (f32) {
+int dense_qmax(int N, int flavor) {
+  if (flavor == 2) {
+#define HMPC_CASE(n) \
+  if (N == n) return qmax_solve_n##n##_f32r();
+    HMPC_F32R_LIST(HMPC_CASE)
+#undef HMPC_CASE
+    return -1;
+  }
+  if (flavor == 1) {
 #define HMPC_CASE(n) \
   if (N == n) return qmax_solve_n##n##_f32();
     HMPC_F32_LIST(HMPC_CASE)
@@ -115,8 +149,15 @@ int dense_qmax(int N, bool f32) {
   return -1;
 }
 
-int dense_split_nv(int N, bool f32) {
-  if (f32) {
+int dense_split_nv(int N, int flavor) {
+  if (flavor == 2) {
+#define HMPC_CASE(n) \
+  if (N == n) return split_nv_n##n##_f32r();
+    HMPC_F32R_LIST(HMPC_CASE)
+#undef HMPC_CASE
+    return 0;
+  }
+  if (flavor == 1) {
 #define HMPC_CASE(n) \
   if (N == n) return split_nv_n##n##_f32();
     HMPC_F32_LIST(HMPC_CASE)
@@ -130,8 +171,15 @@ int dense_split_nv(int N, bool f32) {
   return 0;
 }
 
-const char* dense_name(int variant, int N, bool f32) {
-  if (f32) {
+const char* dense_name(int variant, int N, int flavor) {
+  if (flavor == 2) {
+#define HMPC_CASE(n) \
+  if (N == n) return name_solve_n##n##_f32r(variant);
+    HMPC_F32R_LIST(HMPC_CASE)
+#undef HMPC_CASE
+    return "";
+  }
+  if (flavor == 1) {
 #define HMPC_CASE(n) \
   if (N == n) return name_solve_n##n##_f32(variant);
     HMPC_F32_LIST(HMPC_CASE)

@@ -42,8 +42,10 @@ struct SolveArgs {
   int ws_groups;
   // HMPC_PREC_*: 0 fp64 (fastest kernel for N), 1 fp32 (dense fp32 build
   // where compiled, else generic), 2 fp64 generic, 3 fp64 Riccati, 4 fp64
-  // dense, 5 fp32 generic
+  // dense, 5 fp32 generic, 6 fp32 + fp64 refinement
   int precision;
+  // the fp64 corrections of the refined fp32 build (HMPC_PREC_F32_REFINED)
+  int refine;
   // Active-set overflow (hmpc_ric.hip): an instance whose active set outgrows
   // the LDS capacity of its kernel appends its index to ovf_list (count in
   // *ovf_count; ovf_count[1] is the Riccati instance counter, [2] the
@@ -190,7 +192,7 @@ bool launch_gait(int n_steps, int mpc_factor, int N, double dt, double mpc_dt, d
                  hipStream_t s);
 
 // Which kernel solves (variant, N) at a precision (HMPC_PREC_*).
-enum class Kernel { None, Dense, DenseF32, Riccati, Wide, Cas };
+enum class Kernel { None, Dense, DenseF32, DenseF32R, Riccati, Wide, Cas };
 Kernel pick_kernel(int variant, int N, int precision);
 // Launch the solve kernel for (variant, N, a.precision).  Returns false when
 // no kernel serves that combination.  Dense and Riccati kernels honour
@@ -199,11 +201,12 @@ bool launch_solve(int variant, int N, const SolveArgs& a, hipStream_t stream);
 // the generic-horizon kernel (any 1 <= N <= kWideNmax); a.ws must be set
 bool launch_solve_wide(int variant, int N, const SolveArgs& a, hipStream_t stream);
 // the dedicated dense kernel's active-set capacity (-1: none) and name, as
-// its own object reports them (hmpc_kernels.hip)
-int dense_qmax(int N, bool f32);
+// its own object reports them (hmpc_kernels.hip); flavor 0 fp64, 1 fp32,
+// 2 fp32 + fp64 refinement
+int dense_qmax(int N, int flavor);
 // free-variable bound of the dense split's compacted kernel (0: no split)
-int dense_split_nv(int N, bool f32);
-const char* dense_name(int variant, int N, bool f32);
+int dense_split_nv(int N, int flavor);
+const char* dense_name(int variant, int N, int flavor);
 bool horizon_supported(int variant, int N);   // compiled, or generic (N <= kWideNmax)
 bool horizon_compiled(int variant, int N);    // a dedicated one-wavefront kernel
 int supported_horizons(int variant, int* Ns, int cap);

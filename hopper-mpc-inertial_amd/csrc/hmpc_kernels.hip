@@ -65,6 +65,16 @@ namespace {
 
 using real = HMPC_REAL;
 constexpr bool kF32 = sizeof(real) == 4;
+// fp32 solve + fp64 iterative refinement on its final active set
+// (HMPC_PREC_F32_REFINED, configs[4]): the object is built with
+// -DHMPC_F32_REFINE=1, the number of corrections is a.refine (run time)
+#ifndef HMPC_F32_REFINE
+#define HMPC_F32_REFINE 0
+#endif
+constexpr bool kRefine = kF32 && HMPC_F32_REFINE;
+// the refinement's acceptance: scaled row violations and negative multipliers
+// beyond this send the instance to the fp64 pass
+constexpr double kRefineTol = 1e-9;
 // feasibility tolerance of the slack scan and the relative threshold on
 // |w_perp|^2 for a usable primal direction, per precision
 constexpr real kTolR = kF32 ? real(2e-4) : real(kTol);
@@ -293,8 +303,27 @@ struct Lay {
   static constexpr int LC = U0;                    // M = L diag(L)^-1, column-major packed
   static constexpr int XO = U0;                    // x* staging (after L is dead)
   static constexpr int ENDB = LC + e2(LCN);
-  static constexpr int TOTAL = ENDA > ENDB ? ENDA : ENDB;
+  static constexpr int TOTAL0 = ENDA > ENDB ? ENDA : ENDB;
+  // fp32 + fp64 refinement (HMPC_F32_REFINE builds): an fp64 region after the
+  // rest, offsets in doubles from R64 -- the stage data of gen_dt_dynamics in
+  // fp64 (cos/sin, rows 9..11 of Bd), u in full order, the adjoint rows
+  // 6..11, the rolled-out heights z_k, each lane's full-order slot (int)
+  // Part of it (R64LO) overlays the fp32 stage data CS..ZB, dead once the
+  // active set is final (fp32 builds only run the refinement)
+  static constexpr int R64LO = CS;                   // in reals, 8-B aligned
+  static constexpr int DCS = 0;                      // [N][2]          (R64LO)
+  static constexpr int DU = DCS + 2 * N;             // [6N]            (R64LO)
+  static constexpr int DXZ = DU + NVF;               // [N+1]           (R64LO)
+  static_assert((CS & 1) == 0 && (DXZ + N + 1) * (8 / RB) <= XS - CS, "fp64 overlay");
+  static constexpr int R64 = (TOTAL0 + 1) & ~1;     // in reals, 8-B aligned
+  static constexpr int DBW = 0;                      // [N][3][6]       (R64)
+  static constexpr int DAJ = DBW + 18 * N;           // [N][6]
+  static constexpr int DXR = DAJ + 6 * N;            // [N][12] x_ref
+  static constexpr int DSLOT = DXR + 12 * N;         // [NT] int
+  static constexpr int DTOT = DSLOT + NT / 2;
+  static constexpr int TOTAL = kRefine ? R64 + DTOT * (8 / RB) : TOTAL0;
   static_assert(12 * (N + 1) <= LCN, "x* staging does not fit");
+  static_assert(!kRefine || 24 * (N + 1) + 1 <= LCN, "fp64 x* staging does not fit");
   // start of column k of L (rows k..NV-1)
   __host__ __device__ static constexpr int cb(int k) { return k * NV - ((k * (k - 1)) >> 1); }
 };
@@ -554,6 +583,22 @@ constexpr int waves_of() {   // waves / SIMD the register allocation is held to
        : NVM > 0                      ? 2
                                       : HMPC_WAVES_PER_EU((Lay<N, NVM, QM>::W));
 }
+// The kernel's argument block through an opaque kernarg-segment pointer:
+// reads through it are fresh scalar loads where they stand, so the compiler
+// does not keep the arguments of an early phase alive (in SGPRs, then
+// spilled) until a late phase reads them again.  Device pass only (the host
+// pass merely parses kernel bodies).
+__device__ __forceinline__ const SolveArgs& opaque_args(const SolveArgs& a) {
+#ifdef __HIP_DEVICE_COMPILE__
+  typedef const __attribute__((address_space(4))) SolveArgs karg_t;
+  karg_t* ap = (karg_t*)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(ap));
+  return *(const SolveArgs*)ap;
+#else
+  return a;
+#endif
+}
+
 // One QP instance b, solved by the workgroup (every phase below).  `tid` is
 // threadIdx.x -- in the persistent form an opaque copy made afresh for each
 // instance: the compiler then cannot hoist the lane-derived masks and
@@ -561,6 +606,7 @@ constexpr int waves_of() {   // waves / SIMD the register allocation is held to
 // kernel's life (the Riccati kernel's fix).
 template <int VAR, int N, int NVM, int QM>
 __device__ __forceinline__ void solve_instance(const SolveArgs& a, int64_t b, real* sm, const int tid) {
+  const SolveArgs& a_ = a;
   using L = Lay<N, NVM, QM>;
   static_assert(NVM == 0 || L::W == 1, "the compacted kernel is one wave");
   constexpr int NV = L::NV;
@@ -1534,31 +1580,242 @@ __device__ __forceinline__ void solve_instance(const SolveArgs& a, int64_t b, re
       }
     }
   }
-#if defined(HMPC_REFINE_LB) && HMPC_REFINE_LB > 0
-  // A/B lower bound of fp32 + iterative refinement (configs[4]):
-  // HMPC_REFINE_LB range-space corrections on the final active set -- a
-  // forward sweep, Gram-Schmidt against Qw, a backward sweep each -- scaled by
-  // a run-time zero.  The solve cost a refinement adds before its fp64
-  // residuals (not included); results unchanged.
-  if constexpr (kF32) {
-    const real z0 = sm[L::ZR];
-    real acc = v;
-    const int qu = uni(q);
-#pragma unroll 1
-    for (int it = 0; it < HMPC_REFINE_LB; ++it) {
-      real wp = tri_fwd_lds<L>(tid, acc, Lc, zero, dinv, xs, nf, 0);
-      ladder<0, QMAX>(qu, [&](auto lc) __attribute__((always_inline)) {
-        constexpr int l = decltype(lc)::value;
-        const real cl = B::sum(Qw[l] * wp, red);
-        wp = fma(-cl, Qw[l], wp);
-      });
-      B::sync();
-      const real zi = tri_bwd<L>(tid, wp, Lc, zero, dinv, xs, nf);
-      acc = fma(z0, zi, acc);
-    }
-    v = acc;
-  }
+  // ---------------- fp32 solve + fp64 refinement (kRefine builds) -----------
+  // configs[4]: the fp32 factors and active set, then a.refine
+  // corrections of the KKT system of that active set with fp64 residuals --
+  //   r1 = N_A lam - (H u + h)  (the gradient by an fp64 rollout + adjoint,
+  //        the reference's dynamics rebuilt in fp64 from the fp64 inputs)
+  //   r2 = b_A - N_A' u         (the active rows in fp64)
+  // solved with L^-1 N_A = Qw R: w = L^-1 r1, c = Qw' w, t = R^-T r2,
+  // dlam = R^-1 (t - c), du = L^-T (w - Qw c + Qw t).  An fp64 check of every
+  // row and multiplier then confirms the active set; an instance that fails
+  // it (or any non-solved fp32 instance) goes to the fp64 overflow pass.
+  if constexpr (kRefine) {
+    static_assert(W == 1, "the refinement runs in one-wave kernels");
+#ifdef HMPC_MARKS
+    asm volatile(";@@PHASE 61");
 #endif
+    if (uni(status) != ST_SOLVED && a.ovf_count) status = ST_OVERFLOW;
+    if (uni(status) == ST_SOLVED) {
+      const SolveArgs& a = opaque_args(a_);
+      double* d64 = reinterpret_cast<double*>(sm + L::R64);
+      double* dlo = reinterpret_cast<double*>(sm + L::R64LO);
+      int* dslot = reinterpret_cast<int*>(d64 + L::DSLOT);
+      const double dt64 = a.dt, dtm64 = a.dt / a.m;
+      const double mu64 = a.mu ? a.mu[b] : a.mu_default;
+      const double zc64 = dt64 * dtm64;
+      const double* xrf7 = reinterpret_cast<const double* const*>(sm + L::XRV)[0];
+      const int xrs = reinterpret_cast<const int*>(sm + L::XRV + 2)[0];
+      // gen_dt_dynamics in fp64 (lane k < N: stage k), on the linearisation
+      // rows as phase 0 builds them from the fp64 inputs
+      if (tid < N) {
+        const int k = tid;
+        const double* xp = a.x_lin + b * 12 * (N + 1);
+        const int mode = a.shift_mode;
+        auto xl = [&](int c) -> double {
+          if (mode == 0) return xp[12 * k + c];
+          if (k == 0) return a.x_in[b * 12 + c];
+          return mode == 1 ? xrf7[(k - 1) * xrs + c] : xp[12 * (k + 1 <= N ? k + 1 : N) + c];
+        };
+        const double p3[3] = {xl(0), xl(1), xl(2)};
+        const double* pfp = a.pf + b * a.pf_bs + k * a.pf_rs;
+        const double pf3[3] = {pfp[0], pfp[1], pfp[2]};
+        stage_dynamics_vals<VAR, double>(k, xl(5), p3, pf3, a.Jinv, a.rh, dt64, dlo + L::DCS, d64 + L::DBW);
+      }
+      // u in full order (fixed variables 0), each lane's full-order slot
+      for (int i = tid; i < L::NVF; i += NT) dlo[L::DU + i] = 0.0;
+      dslot[tid] = active_lane ? fidx : 0;
+      for (int i = tid; i < 12 * N; i += NT) {   // x_ref rows
+        const int r = i / 12;
+        d64[L::DXR + i] = xrf7[r * xrs + i - 12 * r];
+      }
+      const double xin64 = a.x_in[b * 12 + (tid < 12 ? tid : 0)];
+      B::sync();
+      double u64 = (double)v;
+      if (active_lane) dlo[L::DU + fidx] = u64;
+      const int qu = uni(q);
+      double lam = tid < qu ? (double)ua[tid] : 0.0;
+      const double qr = qdiag(tid);
+      const int rw = (tid >= 9 && tid < 12) ? tid - 9 : 0;
+      const int rv = (tid >= 6 && tid < 9) ? tid - 6 : 0;
+      const double gdt = tid == 8 ? -a.g * dt64 : 0.0;
+      const double u2mg = 2.0 * a.m * a.g;
+      const double ub_alias = (sm[L::CC + N - 1] != 0.0) ? u2mg : 0.0;
+      B::sync();
+      double dg[N];   // W_k (x_{k+1} - r_k) on lanes < 12
+      // u -> x (fp64, lane r < 12 holds x[r]): dg, the heights z_k and, with
+      // OUT, x* staged at xo and the objective (phase 7's terms)
+      auto rollout = [&](auto outc, double* xo, double& objl) __attribute__((always_inline)) {
+        constexpr bool OUT = decltype(outc)::value;
+        double xr = tid < 12 ? xin64 : 0.0;
+        if (tid == 2) dlo[L::DXZ] = xr;
+        if constexpr (OUT) {
+          if (tid < 12) xo[tid] = xr;
+        }
+        const double rdu = tid < 6 ? kRdiag : 0.0;
+        const int tu = tid < 6 ? tid : 0;
+        sfor<0, N>([&](auto kc) __attribute__((always_inline)) {
+          constexpr int k = decltype(kc)::value;
+          const double cp = dlo[L::DCS + 2 * k], sp = dlo[L::DCS + 2 * k + 1];
+          const double* bwr = d64 + L::DBW + 18 * k + 6 * rw;
+          const double* uk = dlo + L::DU + 6 * k;
+          double bw_u = 0.0;
+#pragma unroll
+          for (int c = 0; c < 6; ++c) bw_u = fma(bwr[c], uk[c], bw_u);
+          double bv_u;
+          if constexpr (VAR == 3) {
+            bv_u = dtm64 * uk[rv];
+          } else {   // Rz' dt/m
+            const double u0 = uk[0], u1 = uk[1], u2 = uk[2];
+            bv_u = (rv == 0) ? dtm64 * (cp * u0 - sp * u1) : ((rv == 1) ? dtm64 * (sp * u0 + cp * u1) : dtm64 * u2);
+          }
+          const double bu = (tid >= 9 && tid < 12) ? bw_u : ((tid >= 6 && tid < 9) ? bv_u : 0.0);
+          xr = ad_lane(xr, dt64, cp, sp, tid) + bu + gdt;
+          const double kf = (k == N - 1) ? kTermQ : 1.0;
+          const double e = xr - d64[L::DXR + 12 * k + (tid < 12 ? tid : 0)];
+          dg[k] = kf * qr * e;
+          if (tid == 2) dlo[L::DXZ + k + 1] = xr;
+          if constexpr (OUT) {
+            objl = fma(kf * qr * e, e, objl);
+            if constexpr (k < N - 1) {
+              const double ub = a.uref_aliased ? ub_alias : ((sm[L::CC + k] != 0.0) ? u2mg : 0.0);
+              const double du = uk[tu] - (tid == 2 ? ub : 0.0);
+              objl = fma(rdu * du, du, objl);
+            }
+            if (tid < 12) xo[12 * (k + 1) + tid] = xr;
+          }
+        });
+      };
+      // constraint id's coefficient on this lane's variable, fp64 (coef_of)
+      auto coef64 = [&](int id) -> double {
+        const int o = id >> 2, sl = id & 3;
+        const int oj = __builtin_amdgcn_readlane(vj, o), oc = __builtin_amdgcn_readlane(vc, o);
+        if (!active_lane) return 0.0;
+        if (oc >= 3) {
+          if (sl == 0) return tid == o ? 1.0 : 0.0;
+          if (sl == 1) return tid == o ? -1.0 : 0.0;
+          if (vc != 2 || vj > oj - 2 || sm[L::CC + vj] == 0.0) return 0.0;
+          return zc64 * (double)(oj - 1 - vj);
+        }
+        if (oc == 2) return tid == o ? (sl == 0 ? 1.0 : -1.0) : 0.0;
+        if (tid == o) return sl == 0 ? -1.0 : 1.0;
+        return (vj == oj && vc == 2) ? mu64 : 0.0;
+      };
+      // n' u - b of constraint id, fp64 (the row at the rolled-out u)
+      auto slack64 = [&](int id) -> double {
+        const int o = id >> 2, sl = id & 3;
+        const int fo = dslot[o], oj = fo / 6, oc = fo - 6 * oj;
+        const double uo = dlo[L::DU + fo], fz = dlo[L::DU + 6 * oj + 2];
+        if (oc >= 3) return sl == 0 ? uo + tau_lim(oc) : (sl == 1 ? tau_lim(oc) - uo : dlo[L::DXZ + oj] - kZmin);
+        if (oc == 2) return sl == 0 ? fz : kFzMax - fz;
+        return sl == 0 ? fma(mu64, fz, -uo) : fma(mu64, fz, uo);
+      };
+      double objl = 0.0;
+      const int nref = a.refine;
+#pragma unroll 1
+      for (int it = 0; it < nref; ++it) {
+        rollout(std::false_type{}, nullptr, objl);
+        // adjoint rows 6..11 (phase 2's recursion on the rollout)
+        {
+          double ar = dg[N - 1];
+          if (tid >= 6 && tid < 12) d64[L::DAJ + 6 * (N - 1) + tid - 6] = ar;
+          sfor<1, N>([&](auto ic) __attribute__((always_inline)) {
+            constexpr int t = N - decltype(ic)::value;
+            ar = adt_lane(ar, dt64, dlo[L::DCS + 2 * t], dlo[L::DCS + 2 * t + 1], tid) + dg[t - 1];
+            if (tid >= 6 && tid < 12) d64[L::DAJ + 6 * (t - 1) + tid - 6] = ar;
+          });
+        }
+        B::sync();
+        // r1 = N_A lam - (H u + h): the gradient 2 Bd' a + 2 V (u - u_ref) (phase 3's h_v at u)
+        double r1 = 0.0;
+        if (active_lane) {
+          const double cpi = dlo[L::DCS + 2 * vj], spi = dlo[L::DCS + 2 * vj + 1];
+          const double* aj = d64 + L::DAJ + 6 * vj;
+          const double* bwi = d64 + L::DBW + 18 * vj;
+          double hacc = 0.0;
+#pragma unroll
+          for (int r = 0; r < 3; ++r) hacc = fma(vc < 3 ? bv<VAR>(r, vc, dtm64, cpi, spi) : 0.0, aj[r], hacc);
+#pragma unroll
+          for (int r = 0; r < 3; ++r) hacc = fma(bwi[6 * r + vc], aj[3 + r], hacc);
+          const double ub = vc == 2 ? (a.uref_aliased ? ub_alias : ((sm[L::CC + vj] != 0.0) ? u2mg : 0.0)) : 0.0;
+          const double Vj = (vj == N - 1) ? 0.0 : kRdiag;
+          r1 = -2.0 * fma(Vj, u64 - ub, hacc);
+        }
+#pragma unroll 1
+        for (int l = 0; l < qu; ++l) r1 = fma(rdlane(lam, l), coef64(act[l]), r1);
+        // r2 = b_A - N_A' u (lane l < q: active row l)
+        const double r2 = tid < qu ? -slack64(act[tid < qu ? tid : 0]) : 0.0;
+        // the correction, on the fp32 factors
+        real w = tri_fwd_lds<L>(tid, (real)r1, Lc, zero, dinv, xs, nf, 0);
+        real cvec = 0;
+        ladder<0, QMAX>(qu, [&](auto lc) __attribute__((always_inline)) {
+          constexpr int l = decltype(lc)::value;
+          const real cl = B::sum(Qw[l] * w, red);
+          w = fma(-cl, Qw[l], w);
+          cvec = tid == l ? cl : cvec;
+        });
+        B::sync();
+        double tcur = r2, tmine = 0.0;   // t = R^-T r2
+#pragma unroll 1
+        for (int l = 0; l < qu; ++l) {
+          const double tl = rdlane(tcur, l) / (double)Rm[loff(l) + l];
+          if (tid == l) tmine = tl;
+          if (tid > l && tid < qu) tcur = fma(-(double)Rm[loff(tid) + l], tl, tcur);
+        }
+        double rcur = tid < qu ? tmine - (double)cvec : 0.0, dlam = 0.0;   // dlam = R^-1 (t - c)
+#pragma unroll 1
+        for (int l = qu - 1; l >= 0; --l) {
+          const double rl = rdlane(rcur, l) / (double)Rm[loff(l) + l];
+          if (tid == l) dlam = rl;
+          if (tid < l) rcur = fma(-(double)Rm[loff(l) + tid], rl, rcur);
+        }
+        real zq = w;   // w - Qw c + Qw t
+        ladder<0, QMAX>(qu, [&](auto lc) __attribute__((always_inline)) {
+          constexpr int l = decltype(lc)::value;
+          zq = fma((real)rdlane(tmine, l), Qw[l], zq);
+        });
+        const real du = tri_bwd<L>(tid, zq, Lc, zero, dinv, xs, nf);
+        u64 += active_lane ? (double)du : 0.0;
+        lam += dlam;
+        if (active_lane) dlo[L::DU + fidx] = u64;
+        B::sync();
+      }
+      // outputs: x* (staged over L, dead now) and the objective from an fp64
+      // rollout of the refined u
+      double* xo = reinterpret_cast<double*>(sm + ((L::XO + 1) & ~1));
+      rollout(std::true_type{}, xo, objl);
+      const double objv = wave_sum(objl);
+      // the fp64 check: every row of this lane (slots as in the slack scan,
+      // scaled by the row norms) and the multipliers
+      double worst = INFINITY;
+      if (active_lane) {
+        const int id0 = 4 * tid;
+        if (vc >= 3) {
+          worst = fmin(slack64(id0), slack64(id0 + 1));
+          if (vc == 3 && vj >= 2 && znorm > 0) worst = fmin(worst, slack64(id0 + 2) / (double)znorm);
+        } else if (sm[L::CC + vj] != 0.0 && !(VAR == 2 && vc == 1)) {
+          const double sc = vc == 2 ? 1.0 : 1.0 / sqrt(1.0 + mu64 * mu64);
+          worst = fmin(slack64(id0), slack64(id0 + 1)) * sc;
+        }
+      }
+      const bool bad = __ballot(worst < -kRefineTol || (tid < qu && lam < -kRefineTol)) != 0;
+      if (bad) {
+        status = a.ovf_count ? ST_OVERFLOW : ST_NUMERICAL;
+      } else {
+        B::sync();
+        if (tid < L::NVF) a.u[b * L::NVF + tid] = dlo[L::DU + tid];
+        if (a.x)
+          for (int i = tid; i < 12 * (N + 1); i += NT) a.x[b * 12 * (N + 1) + i] = xo[i];
+        if (tid == 0) {
+          if (a.obj) a.obj[b] = objv;
+          a.status[b] = ST_SOLVED;
+          if (a.iters) a.iters[b] = iters;
+          if (a.active) a.active[b] = q;
+        }
+        return;
+      }
+    }
+  }
   HMPC_STAMP(7);
   if constexpr (HMPC_PRIO != 0) __builtin_amdgcn_s_setprio(kCmpCls ? 0 : HMPC_PRIO_FULL_BASE);
 
@@ -1569,6 +1826,10 @@ __device__ __forceinline__ void solve_instance(const SolveArgs& a, int64_t b, re
       a.status[b] = ST_OVERFLOW;
       a.ovf_list[atomicAdd(a.ovf_count, 1)] = (int32_t)b;
     }
+    return;
+  }
+  if constexpr (kRefine) {   // (no fp64 pass to hand it to: the status alone)
+    if (tid == 0) a.status[b] = status == ST_SOLVED ? ST_NUMERICAL : status;
     return;
   }
 
@@ -1802,7 +2063,13 @@ bool launch_class(K kern, const SolveArgs& a, hipStream_t s) {
 // blocks past the list's length exit).  HMPC_SPLIT_PERSIST=0 builds the
 // latter (A/B).
 #ifndef HMPC_SPLIT_PERSIST
-#define HMPC_SPLIT_PERSIST 1
+#define HMPC_SPLIT_PERSIST 0
+#endif
+// 1: the full class on the high-priority split stream, the compacted one on
+// the caller's; 0: the full class on the caller's stream, the compacted one on
+// a split stream of the same priority (hmpc_capi.cpp creates them)
+#ifndef HMPC_SPLIT_PRIO
+#define HMPC_SPLIT_PRIO 0
 #endif
 #if HMPC_SPLIT_PERSIST
 #define HMPC_CLASS_LAUNCH(...) launch_class(solve_kernel_p<__VA_ARGS__>, a, s)
@@ -1888,16 +2155,22 @@ bool HMPC_CAT(HMPC_CAT(launch_solve_n, HMPC_INST_N), HMPC_LAUNCH_SUFFIX)(int var
     const bool fork = a.split_fork && (a.split_stream[0] || a.split_stream[1]);
     if (fork && hipEventRecord(a.split_fork, s) != hipSuccess) return false;
     hipStream_t t0 = fork ? a.split_stream[0] : s, t1 = fork ? a.split_stream[1] : s;
-    if (!on_stream(s, t0, a.split_fork, a.split_join[0], [&](hipStream_t t) {
-          return variant == 3 ? launch_full3f(afl, t)
+    auto full = [&](hipStream_t t) {
+      return variant == 3 ? launch_full3f(afl, t)
 #ifdef HMPC_FULL2F_NV
-                              : HMPC_CAT(launch_full2f_n, HMPC_INST_N)(afl, t);
+                          : HMPC_CAT(launch_full2f_n, HMPC_INST_N)(afl, t);
 #else
-                              : (hipLaunchKernelGGL((solve_kernel<2, N, real>), dim3((unsigned)a.B), dim3(NT), 0, t, afl), true);
+                          : (hipLaunchKernelGGL((solve_kernel<2, N, real>), dim3((unsigned)a.B), dim3(NT), 0, t, afl), true);
 #endif
-        }))
-      return false;
-    if (!HMPC_CAT(launch_cmp_n, HMPC_INST_N)(variant, ac, s)) return false;
+    };
+    auto cmp = [&](hipStream_t t) { return HMPC_CAT(launch_cmp_n, HMPC_INST_N)(variant, ac, t); };
+#if HMPC_SPLIT_PRIO
+    if (!on_stream(s, t0, a.split_fork, a.split_join[0], full)) return false;
+    if (!cmp(s)) return false;
+#else   // the full class on the caller's stream, the compacted one forked (same priority)
+    if (!full(s)) return false;
+    if (!on_stream(s, t0, a.split_fork, a.split_join[0], cmp)) return false;
+#endif
 #if HMPC_SML_NV > 0
     const SolveArgs asm_ = cls(2);
     if (!on_stream(s, t1, a.split_fork, a.split_join[1],

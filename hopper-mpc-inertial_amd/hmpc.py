@@ -21,7 +21,8 @@ ERRORS = {-1: 'HMPC_ERR_ARG', -2: 'HMPC_ERR_UNSUPPORTED', -3: 'HMPC_ERR_HIP', -4
 STATUS = {0: 'solved', 1: 'max_iter', 2: 'primal_infeasible', 3: 'numerical'}
 VARIANTS = {'3f': 3, '2f': 2, 'cas': 4, 3: 3, 2: 2, 4: 4}
 UREF = {'aliased': 0, 'per_stage': 1}
-PRECISION = {'f64': 0, 'f32': 1, 'f64_generic': 2, 'f64_riccati': 3, 'f64_dense': 4, 'f32_generic': 5}
+PRECISION = {'f64': 0, 'f32': 1, 'f64_generic': 2, 'f64_riccati': 3, 'f64_dense': 4, 'f32_generic': 5,
+             'f32_refined': 6}
 
 # symbol -> (restype, argtypes); every symbol declared in include/hmpc.h
 _D = ctypes.POINTER(ctypes.c_double)
@@ -36,6 +37,7 @@ SIGNATURES = {
     'hmpc_destroy': (ctypes.c_int, [_VP]),
     'hmpc_solve_batch': (ctypes.c_int, [_VP, ctypes.c_int64] + [_VP] * 11 + [_VP]),
     'hmpc_solve_batch_stats': (ctypes.c_int, [_VP, ctypes.c_int64] + [_VP] * 12 + [_VP]),
+    'hmpc_set_refinement': (ctypes.c_int, [_VP, ctypes.c_int]),
     'hmpc_solve_batch_host': (ctypes.c_int, [_VP, ctypes.c_int64] + [_VP] * 11),
     'hmpc_mpcontrol_batch': (ctypes.c_int, [_VP, ctypes.c_int64, ctypes.c_int] + [_VP] * 10 + [_VP]),
     'hmpc_mpcontrol_plan_batch': (ctypes.c_int, [_VP, ctypes.c_int64, ctypes.c_int, _VP, _VP, _VP,
@@ -156,6 +158,10 @@ class Context:
         self._lib = lib
         if precision != 'f64':
             self._check(lib.hmpc_set_precision(h, PRECISION[precision]), 'hmpc_set_precision')
+
+    def set_refinement(self, corrections):
+        """fp64 corrections of precision 'f32_refined' (hmpc_set_refinement)."""
+        self._check(self._lib.hmpc_set_refinement(self._h, int(corrections)), 'hmpc_set_refinement')
 
     @property
     def kernel_name(self):

@@ -86,13 +86,18 @@ extern "C" {
 #define HMPC_PREC_F64_DENSE 4     /* fp64 on the dedicated dense kernel of N (compiled
                                      horizons only; the default for N <= 10)      */
 #define HMPC_PREC_F32_GENERIC 5   /* fp32 on the generic kernel (round-1 configs[4]) */
+#define HMPC_PREC_F32_REFINED 6   /* configs[4]'s fp32 + fp64 iterative refinement: the fp32
+                                     dense kernel's factors and active set, then
+                                     hmpc_set_refinement() corrections of that active set's
+                                     KKT system with fp64 residuals; an instance whose fp64
+                                     check fails goes to the fp64 overflow pass (N = 10) */
 
 typedef struct hmpc_ctx hmpc_ctx;
 
 /* ABI version (major*10000 + minor*100 + patch): 1.2.0 = 1.0 + the fp32 dense
    build, HMPC_PREC_F64_RICCATI / _F64_DENSE / _F32_GENERIC, hmpc_kernel_name,
    hmpc_active_capacity, hmpc_plan_batch, hmpc_gait_batch, HMPC_VARIANT_CAS;
-   1.3.0 = + hmpc_solve_batch_stats */
+   1.3.0 = + hmpc_solve_batch_stats, HMPC_PREC_F32_REFINED, hmpc_set_refinement */
 int hmpc_version(void);
 
 /* Which horizons have a dedicated (one- or two-wavefront) kernel for
@@ -233,11 +238,15 @@ int hmpc_gait_batch(hmpc_ctx* ctx, int n_steps, int mpc_factor, int N, double dt
    (reduced Hessian condition ~3e6), see DESIGN.md. */
 int hmpc_set_precision(hmpc_ctx* ctx, int precision);
 
+/* Number of fp64 corrections HMPC_PREC_F32_REFINED runs (0..16, default 2;
+   each costs an fp64 rollout + adjoint and two fp32 sweeps per instance). */
+int hmpc_set_refinement(hmpc_ctx* ctx, int corrections);
+
 /* Name of the solve kernel this context's (variant, N, precision) runs on,
    as rocprofv3 demangles it, e.g. "hmpc::ric_kernel<3, 2, 0, 0>"; a split launch names
-   both kernels, "hmpc::solve_kernel<3, 10, double, 48, 13> + hmpc::solve_kernel<3, 10,
-   double, 0, 0>" (the compacted one first; 2f's full class is the 5N-wide
-   "hmpc::solve_kernel<2, 10, double, 50, 20>").  Static string, "" when none.  For
+   every class kernel, "hmpc::solve_kernel_p<3, 10, double, 48, 13> + hmpc::solve_kernel_p<3, 10,
+   double, 0, 0>" (the narrowest first; 2f's full class is the 5N-wide
+   "hmpc::solve_kernel_p<2, 10, double, 50, 20>").  Static string, "" when none.  For
    benchmark records and profiles. */
 const char* hmpc_kernel_name(hmpc_ctx* ctx);
 

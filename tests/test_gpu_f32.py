@@ -25,11 +25,13 @@ def hm():
     return hmpc
 
 
-def solve(hm, precision, inst, N=10, variant='3f'):
+def solve(hm, precision, inst, N=10, variant='3f', refine=None):
     import hmpc_plan
     c = hmpc_plan.runner_constants()
     cx = hm.Context(variant, N, t=c['t'], m=c['m'], g=c['g'], mu=1.0, Jinv=c['Jinv'], rh=c['rh'],
                     precision=precision)
+    if refine is not None:
+        cx.set_refinement(refine)
     name = cx.kernel_name
     r = cx.solve_host(inst['x_in'], inst['x_lin'], inst['x_ref'], inst['pf'], inst['C'], mu=inst['mu'])
     cx.close()
@@ -77,3 +79,44 @@ def test_fp32_dense_overflow_goes_to_the_fp64_pass(hm):
     assert (g['status'] == 0).all()
     du = np.abs(g['u'] - ref['u']).max(axis=(1, 2))
     assert (du <= 1e-6).any()   # the overflowed ones, solved in fp64
+
+
+@pytest.mark.parametrize('variant,curve,musweep', [('3f', True, False), ('3f', False, True),
+                                                   ('2f', False, False)])
+def test_fp32_refined_meets_the_fp64_tolerance(hm, variant, curve, musweep):
+    """HMPC_PREC_F32_REFINED (configs[4]): the fp32 kernel's factors and active
+    set, then 3 corrections with fp64 residuals (an fp64 rollout + adjoint of
+    the reference's dynamics rebuilt from the fp64 inputs); instances whose
+    fp64 check fails are re-solved by the fp64 pass.  Every instance matches
+    the exact optimum like the fp64 kernel: |du| <= 1e-6, objective 1e-9."""
+    import hmpc_plan
+    from oracle import port
+    N, B = 10, 1024
+    inst = hmpc_plan.sample_instances(B, N, curve=curve, seed=93,
+                                      mu_sweep=(0.3, 1.2) if musweep else None)
+    g, name = solve(hm, 'f32_refined', inst, N, variant, refine=3)
+    assert name == f'hmpc::solve_kernel<{variant[0]}, 10, float, 0, 0>'
+    ref = port.solve_batch(variant, N, inst['x_in'], inst['x_lin'], inst['x_ref'], inst['pf'], inst['C'],
+                           mu=inst['mu'], nthreads=16)
+    assert np.array_equal(g['status'], ref['status'])
+    ok = ref['status'] == 0
+    du = np.abs(g['u'][ok] - ref['u'][ok]).max()
+    assert du <= 1e-6, du
+    rel = np.abs(g['obj'][ok] - ref['obj'][ok]) / np.abs(ref['obj'][ok])
+    assert rel.max() <= 1e-9, rel.max()
+    assert np.abs(g['x'][ok] - ref['x'][ok]).max() <= 1e-6
+
+
+def test_fp32_refined_two_corrections(hm):
+    """Two corrections: statuses equal, |du| within 1e-4 (the convergence
+    model: 1.3e-5 on the worst instance), recorded for the bench's trade-off."""
+    import hmpc_plan
+    from oracle import port
+    N, B = 10, 1024
+    inst = hmpc_plan.sample_instances(B, N, curve=True, seed=94)
+    g, _ = solve(hm, 'f32_refined', inst, N, '3f', refine=2)
+    ref = port.solve_batch('3f', N, inst['x_in'], inst['x_lin'], inst['x_ref'], inst['pf'], inst['C'],
+                           mu=inst['mu'], nthreads=16)
+    assert np.array_equal(g['status'], ref['status'])
+    ok = ref['status'] == 0
+    assert np.abs(g['u'][ok] - ref['u'][ok]).max() <= 1e-4
