@@ -20,27 +20,20 @@ F32LIST=""
 for n in $F32_HORIZONS; do F32LIST="$F32LIST X($n)"; done
 pids=()
 # the split launch's compacted kernel (at most NV free variables, active-set
-# capacity Q, 3 waves / SIMD) and optionally a narrow third class (at most NS
-# free variables) per horizon: "N:NV:Q[:NS]" (CMP="" disables the split)
+# capacity Q, 3 waves / SIMD) per horizon: "N:NV:Q" (CMP="" disables)
 CMP=${CMP-"10:48:13"}
 cmp_flags() {
   for e in $CMP; do
-    IFS=: read -r cn cv cq cs <<< "$e"
-    if [ "$cn" = "$1" ]; then echo "-DHMPC_CMP_NV=$cv -DHMPC_CMP_Q=$cq ${cs:+-DHMPC_SML_NV=$cs}"; fi
+    IFS=: read -r cn cv cq <<< "$e"
+    if [ "$cn" = "$1" ]; then echo "-DHMPC_CMP_NV=$cv -DHMPC_CMP_Q=$cq"; fi
   done
 }
-# The split's persistent class kernels loop over their instances.  Machine
-# LICM would hoist every compile-time lane mask and constant of the unrolled
-# body (hundreds of s_movs) out of that loop and hold them for the kernel's
-# life: SGPR spills into VGPR lanes, then scratch (556 B/lane in the
-# compacted class; 40 B without it).  Off for the split horizons' objects.
-SPLIT_FLAGS=${SPLIT_FLAGS-""}   # "-mllvm -disable-machine-licm" with -DHMPC_SPLIT_PERSIST=1
 CMPOBJS=""
 for n in $HORIZONS; do
-  $HIPCC $FLAGS -DHMPC_INST_N=$n $(cmp_flags $n) $([ -n "$(cmp_flags $n)" ] && echo $SPLIT_FLAGS) -c ${KSRC:-csrc/hmpc_kernels.hip} -o $BDIR/hmpc_kernels_n$n.o "$@" &
+  $HIPCC $FLAGS -DHMPC_INST_N=$n $(cmp_flags $n) -c ${KSRC:-csrc/hmpc_kernels.hip} -o $BDIR/hmpc_kernels_n$n.o "$@" &
   pids+=($!)
-  if [ -n "$(cmp_flags $n)" ]; then   # the compacted class: a translation unit of its own
-    $HIPCC $FLAGS -DHMPC_INST_N=$n $(cmp_flags $n) $SPLIT_FLAGS -DHMPC_CMP_ONLY -c ${KSRC:-csrc/hmpc_kernels.hip} -o $BDIR/hmpc_kernels_n${n}_cmp.o "$@" &
+  if [ -n "$(cmp_flags $n)" ]; then   # the compacted kernel: a translation unit of its own
+    $HIPCC $FLAGS -DHMPC_INST_N=$n $(cmp_flags $n) -DHMPC_CMP_ONLY -c ${KSRC:-csrc/hmpc_kernels.hip} -o $BDIR/hmpc_kernels_n${n}_cmp.o "$@" &
     pids+=($!)
     CMPOBJS="$CMPOBJS $BDIR/hmpc_kernels_n${n}_cmp.o"
   fi

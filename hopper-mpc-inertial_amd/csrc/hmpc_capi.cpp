@@ -36,21 +36,19 @@ struct hmpc_ctx {
   double* wsbuf = nullptr;
   int wsgroups = 0;
   // active-set overflow pass (hmpc_ric.hip): [overflow count | Riccati
-  // instance counter | done counter | split counts (3) | split claim counters
-  // (3) | pad (7) | list of ovf_cap ids] and the global R blocks of its
-  // workgroups
+  // instance counter | done counter | split counts (2) | pad (3) | list of
+  // ovf_cap ids] and the global R blocks of its workgroups
   int32_t* ovf = nullptr;
   int64_t ovf_cap = 0;
   // the counters need a zeroing before the next solve (fresh buffer, or a
   // solve whose overflow pass -- which zeroes them at its end -- did not run)
   bool ovf_dirty = true;
   double* rws = nullptr;
-  // dense split launch: the class lists [3][split_cap], the streams of the
-  // full (high priority) and narrow (low priority) classes
+  // dense split launch: the two class lists [2][split_cap]
   int32_t* split = nullptr;
   int64_t split_cap = 0;
-  hipStream_t split_stream[2] = {nullptr, nullptr};
-  hipEvent_t split_fork = nullptr, split_join[2] = {nullptr, nullptr};
+  hipStream_t split_stream = nullptr;   // the compacted class's stream
+  hipEvent_t split_fork = nullptr, split_join = nullptr;
   // Riccati kernel: per-workgroup K / Dinv workspace of its resident grid
   double* kws = nullptr;
   int ric_groups = 0;
@@ -99,10 +97,8 @@ hmpc::SolveArgs make_args(hmpc_ctx* c, int64_t B, const double* x_in, const doub
   a.ws = nullptr; a.ws_stride = 0; a.ws_groups = 0;
   a.ovf_count = nullptr; a.ovf_list = nullptr; a.rws = nullptr; a.rws_stride = 0;
   a.work = nullptr; a.kws = nullptr; a.kws_stride = 0; a.ric_groups = 0;
-  a.split_count = nullptr; a.split_list = nullptr; a.list = nullptr; a.list_count = nullptr; a.list_work = nullptr;
-  a.split_stream[0] = a.split_stream[1] = nullptr;
-  a.split_fork = nullptr;
-  a.split_join[0] = a.split_join[1] = nullptr;
+  a.split_count = nullptr; a.split_list = nullptr; a.list = nullptr; a.list_count = nullptr;
+  a.split_stream = nullptr; a.split_fork = nullptr; a.split_join = nullptr;
   a.precision = c->precision;
   a.refine = c->refine;
   return a;
@@ -143,7 +139,7 @@ int prepare_ws(hmpc_ctx* c, int64_t B, hmpc::SolveArgs& a) {
 // active set outgrew the main kernel's capacity.
 constexpr int kOvfGroups = 128;
 // ints before the overflow list in the counter buffer (see hmpc_ctx::ovf)
-constexpr int kOvfHeader = 16;
+constexpr int kOvfHeader = 8;
 
 // Buffers of the dense / Riccati kernels: [overflow count | instance counter |
 // pad | overflow list], the overflow pass's blocks, the Riccati kernel's
@@ -194,45 +190,31 @@ int prepare_ric(hmpc_ctx* c, int64_t B, hmpc::SolveArgs& a) {
   a.ovf_count = c->ovf;
   a.work = c->ovf + 1;
   a.ovf_list = c->ovf + kOvfHeader;
-  // the dense kernel's split launch (narrower kernels for the instances with
-  // few free variables): class counts and claim counters next to the
-  // overflow counters, which the overflow pass zeroes together at its end
+  // the dense kernel's split launch (compacted kernel for the instances with
+  // few free variables): class counts next to the overflow counters, which
+  // the overflow pass zeroes together at its end
   if (k == hmpc::Kernel::Dense && hmpc::dense_split_nv(c->N, 0) > 0) {
     if (B > c->split_cap) {
       if (c->split) (void)hipFree(c->split);
       c->split = nullptr;
       c->split_cap = 0;
-      hipError_t e = hipMalloc(&c->split, sizeof(int32_t) * 3 * (size_t)B);
+      hipError_t e = hipMalloc(&c->split, sizeof(int32_t) * 2 * (size_t)B);
       if (e != hipSuccess) { c->err = "split list hipMalloc"; return HMPC_ERR_NOMEM; }
       c->split_cap = B;
     }
-    if (!c->split_fork) {
-      int least = 0, greatest = 0;
-#ifndef HMPC_SPLIT_PRIO
-#define HMPC_SPLIT_PRIO 0
-#endif
-      if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) {
-        c->err = "stream priority range";
-        return HMPC_ERR_HIP;
-      }
-      if (!HMPC_SPLIT_PRIO) least = greatest = 0;
-      if (
-          hipStreamCreateWithPriority(&c->split_stream[0], hipStreamNonBlocking, greatest) != hipSuccess ||
-          hipStreamCreateWithPriority(&c->split_stream[1], hipStreamNonBlocking, least) != hipSuccess ||
-          hipEventCreateWithFlags(&c->split_join[0], hipEventDisableTiming) != hipSuccess ||
-          hipEventCreateWithFlags(&c->split_join[1], hipEventDisableTiming) != hipSuccess ||
-          hipEventCreateWithFlags(&c->split_fork, hipEventDisableTiming) != hipSuccess) {
-        c->err = "split streams / events";
+    if (!c->split_stream) {
+      if (hipStreamCreateWithFlags(&c->split_stream, hipStreamNonBlocking) != hipSuccess ||
+          hipEventCreateWithFlags(&c->split_fork, hipEventDisableTiming) != hipSuccess ||
+          hipEventCreateWithFlags(&c->split_join, hipEventDisableTiming) != hipSuccess) {
+        c->err = "split stream / events";
         return HMPC_ERR_HIP;
       }
     }
     a.split_count = c->ovf + 3;
     a.split_list = c->split;
-    a.split_stream[0] = c->split_stream[0];
-    a.split_stream[1] = c->split_stream[1];
+    a.split_stream = c->split_stream;
     a.split_fork = c->split_fork;
-    a.split_join[0] = c->split_join[0];
-    a.split_join[1] = c->split_join[1];
+    a.split_join = c->split_join;
   }
   a.rws = c->rws;
   a.rws_stride = rstride;
@@ -264,7 +246,7 @@ int run_solve(hmpc_ctx* c, hmpc::SolveArgs a, hipStream_t s) {
   // next solve's kernels see them zero).  The CasADi kernel has no overflow
   // pass.
   if (a.work && (!a.ovf_count || c->ovf_dirty)) {
-    hipError_t e = hipMemsetAsync(a.work - 1, 0, (a.ovf_count ? 9 : 3) * sizeof(int32_t), s);
+    hipError_t e = hipMemsetAsync(a.work - 1, 0, (a.ovf_count ? 5 : 3) * sizeof(int32_t), s);
     if (e != hipSuccess) return fail_hip(c, e, "hipMemsetAsync(overflow count)");
   }
   c->ovf_dirty = true;   // until the overflow pass is launched
@@ -380,11 +362,9 @@ int hmpc_destroy(hmpc_ctx* c) {
   if (c->ovf) (void)hipFree(c->ovf);
   if (c->rws) (void)hipFree(c->rws);
   if (c->split) (void)hipFree(c->split);
-  for (int i = 0; i < 2; ++i) {
-    if (c->split_stream[i]) (void)hipStreamDestroy(c->split_stream[i]);
-    if (c->split_join[i]) (void)hipEventDestroy(c->split_join[i]);
-  }
+  if (c->split_stream) (void)hipStreamDestroy(c->split_stream);
   if (c->split_fork) (void)hipEventDestroy(c->split_fork);
+  if (c->split_join) (void)hipEventDestroy(c->split_join);
   if (c->kws) (void)hipFree(c->kws);
   if (c->plan_scratch) (void)hipFree(c->plan_scratch);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);

@@ -64,24 +64,19 @@ struct SolveArgs {
   double* kws;
   int64_t kws_stride;
   // Dense split launch (hmpc_kernels.hip, objects built with HMPC_CMP_NV):
-  // [compacted | full | narrow count | their three claim counters] (zero at
-  // the launch, zeroed again by the overflow pass at its end) and the class
-  // lists [3][B]; nullptr = one launch of the full kernel.  list / list_count: set per launch by the
+  // [compacted count | full count] (zero at the launch, zeroed again by the
+  // overflow pass at its end) and the two class lists [2][B]; nullptr = one
+  // launch of the full kernel.  list / list_count: set per launch by the
   // launcher (the kernel's class list), nullptr = block i solves instance i.
   int32_t* split_count;
   int32_t* split_list;
   const int32_t* list;
   const int32_t* list_count;
-  // persistent class kernels (solve_kernel_p): the class list's claim
-  // counter (zero at the launch, zeroed again by the overflow pass)
-  int32_t* list_work;
-  // the split's classes run concurrently: the full class on split_stream[0]
-  // (high priority), the compacted one on the caller's stream, the narrow one
-  // on split_stream[1] (low priority), forked from the caller's stream after
-  // the classify pass and joined back into it by the events; nullptr: every
-  // class on the caller's stream, one after the other
-  hipStream_t split_stream[2];
-  hipEvent_t split_fork, split_join[2];
+  // the split's second class runs concurrently on split_stream (forked from
+  // and joined back into the caller's stream by the two events); nullptr:
+  // both classes on the caller's stream, one after the other
+  hipStream_t split_stream;
+  hipEvent_t split_fork, split_join;
 };
 
 // The Riccati kernel (hmpc_ric.hip): any horizon 1 <= N <= kRicNmax, one

@@ -368,10 +368,11 @@ __device__ __forceinline__ void sweep_stage(real b, real& a0, real& a1, real* bu
 // and the sweep starts there (constraint normals are sparse: a box or
 // friction row of stage j starts at 6j).
 template <class L>
-__device__ __forceinline__ real tri_fwd_lds(const int tid, real acc, const real* Mc, const real* zero,
+__device__ __forceinline__ real tri_fwd_lds(real acc, const real* Mc, const real* zero,
                                               real dinv, real* red, int nf, int s0 = 0) {
   constexpr int NV = L::NV;
   constexpr int SEND = L::W == 1 ? (NV + 3) & ~3 : ((NV + kRing2 - 1) / kRing2) * kRing2;   // padded (steps >= NV are no-ops)
+  const int tid = threadIdx.x;
   if constexpr (L::W == 1) {
     // M[tid][s] for tid > s sits at Mc[cb(s) + tid - s]; other lanes read a 0
     // (the lane mask is built on the scalar unit: no v_cmp per step)
@@ -446,11 +447,12 @@ __device__ __forceinline__ real tri_fwd_lds(const int tid, real acc, const real*
 // z = L^-T b (lane v holds b_v), M from the LDS copy.  One wave: loads of
 // step s-4 are issued at step s (a 4-deep ring of hand-counted loads).
 template <class L>
-__device__ __forceinline__ real tri_bwd(const int tid, real acc, const real* Mc, const real* zero,
+__device__ __forceinline__ real tri_bwd(real acc, const real* Mc, const real* zero,
                                           real dinv, real* red, int nf) {
   constexpr int NV = L::NV;
   // first step, padded to the ring (steps >= nf are no-ops)
   const int STOP = L::W == 1 ? ((nf + kRing1 - 1) & ~(kRing1 - 1)) - 1 : ((NV + 3) & ~3) - 1;
+  const int tid = threadIdx.x;
   const int cbt = tid < NV ? L::cb(tid) : 0;
   acc *= dinv;
   if constexpr (L::W == 1) {
@@ -568,21 +570,6 @@ __device__ __forceinline__ real tri_bwd(const int tid, real acc, const real* Mc,
 // the widest compacted rows that fit 3 waves / SIMD (<= 168 VGPRs); a wider
 // compacted kernel (2f's 5N-wide full class) runs 2 waves like the full one
 constexpr int kCmp3W = 48;
-// the split's narrow third class (nf <= HMPC_SML_NV; 0: none) and its waves
-// per SIMD
-#ifndef HMPC_SML_NV
-#define HMPC_SML_NV 0
-#endif
-#ifndef HMPC_SML_WAVES
-#define HMPC_SML_WAVES 4
-#endif
-template <int N, int NVM, int QM>
-constexpr int waves_of() {   // waves / SIMD the register allocation is held to
-  return NVM > 0 && NVM <= HMPC_SML_NV ? HMPC_SML_WAVES
-       : NVM > 0 && NVM <= kCmp3W     ? HMPC_CMP_WAVES
-       : NVM > 0                      ? 2
-                                      : HMPC_WAVES_PER_EU((Lay<N, NVM, QM>::W));
-}
 // The kernel's argument block through an opaque kernarg-segment pointer:
 // reads through it are fresh scalar loads where they stand, so the compiler
 // does not keep the arguments of an early phase alive (in SGPRs, then
@@ -599,14 +586,12 @@ __device__ __forceinline__ const SolveArgs& opaque_args(const SolveArgs& a) {
 #endif
 }
 
-// One QP instance b, solved by the workgroup (every phase below).  `tid` is
-// threadIdx.x -- in the persistent form an opaque copy made afresh for each
-// instance: the compiler then cannot hoist the lane-derived masks and
-// addresses out of the instance loop and hold them (spilled) for the
-// kernel's life (the Riccati kernel's fix).
-template <int VAR, int N, int NVM, int QM>
-__device__ __forceinline__ void solve_instance(const SolveArgs& a, int64_t b, real* sm, const int tid) {
-  const SolveArgs& a_ = a;
+template <int VAR, int N, typename R, int NVM = 0, int QM = 0>
+__global__ void __launch_bounds__((Lay<N, NVM, QM>::NT),
+                                  (NVM > 0 && NVM <= kCmp3W ? HMPC_CMP_WAVES
+                                   : (NVM > 0 ? 2 : HMPC_WAVES_PER_EU((Lay<N, NVM, QM>::W)))))
+solve_kernel(SolveArgs a) {
+  static_assert(sizeof(R) == sizeof(real), "one arithmetic type per build");
   using L = Lay<N, NVM, QM>;
   static_assert(NVM == 0 || L::W == 1, "the compacted kernel is one wave");
   constexpr int NV = L::NV;
@@ -614,6 +599,7 @@ __device__ __forceinline__ void solve_instance(const SolveArgs& a, int64_t b, re
   constexpr int NT = L::NT;
   constexpr int QMAX = L::QMAX;
   using B = Blk<W>;
+  __shared__ __attribute__((aligned(16))) real sm[L::TOTAL];
   real* red = sm + L::RED;
   real* xs = sm + L::XS;
 #ifdef HMPC_STAMPS
@@ -623,6 +609,14 @@ __device__ __forceinline__ void solve_instance(const SolveArgs& a, int64_t b, re
   constexpr bool kCmpCls = NVM > 0 && NVM <= kCmp3W;   // the split's compacted class
   if constexpr (HMPC_PRIO_FULL_BASE != 0 && !kCmpCls) __builtin_amdgcn_s_setprio(HMPC_PRIO_FULL_BASE);
 
+  const int tid = threadIdx.x;
+  // split launch (launch_solve_n<N>): block i solves the i-th instance of this
+  // kernel's class list; blocks beyond the list's length have no work
+  int64_t b = blockIdx.x;
+  if (a.list) {
+    if ((int)blockIdx.x >= *a.list_count) return;
+    b = a.list[blockIdx.x];
+  }
   const real dt = a.dt;
   const real dtm = dt / real(a.m);
 
@@ -811,7 +805,7 @@ __device__ __forceinline__ void solve_instance(const SolveArgs& a, int64_t b, re
     sfor<0, N>([&](auto kc) __attribute__((always_inline)) {
       constexpr int k = decltype(kc)::value;
       const real cp = rdlane(cpl, k), sp = rdlane(spl, k);
-      xr = ad_lane(xr, dt, cp, sp, tid) + ((tid == 8) ? -real(a.g) * dt : real(0));
+      xr = ad_lane(xr, dt, cp, sp) + ((tid == 8) ? -real(a.g) * dt : real(0));
       const real kf = (k == N - 1) ? kTermQ : 1.0;
       dgv[k] = kf * qr * (xr - xrf[k]);   // 0 on lanes >= 12 (qr = 0)
       if (tid == 2) sm[L::ZB + k + 1] = xr;
@@ -855,7 +849,7 @@ __device__ __forceinline__ void solve_instance(const SolveArgs& a, int64_t b, re
     if (tid >= 6 && tid < 12) sm[L::AJ + 6 * (N - 1) + tid - 6] = ar;
     sfor<1, N>([&](auto ic) __attribute__((always_inline)) {
       constexpr int t = N - decltype(ic)::value;   // N-1 .. 1
-      ar = adt_lane(ar, dt, rdlane(cpl, t), rdlane(spl, t), tid) + dgv[t - 1];
+      ar = adt_lane(ar, dt, rdlane(cpl, t), rdlane(spl, t)) + dgv[t - 1];
       if (tid >= 6 && tid < 12) sm[L::AJ + 6 * (t - 1) + tid - 6] = ar;
     });
   }
@@ -1276,7 +1270,7 @@ __device__ __forceinline__ void solve_instance(const SolveArgs& a, int64_t b, re
   {
     real y;
     y = wv * dinv;   // L^-1 (-h), swept during the Cholesky
-    v = tri_bwd<L>(tid, y, Lc, zero, dinv, xs, nf);
+    v = tri_bwd<L>(y, Lc, zero, dinv, xs, nf);
   }
   HMPC_STAMP(6);
 
@@ -1431,7 +1425,7 @@ __device__ __forceinline__ void solve_instance(const SolveArgs& a, int64_t b, re
     // w = L^-1 n_p
     HMPC_TIC(t_fwd);
     const int s0 = B::first(np_me != 0.0, red);   // first nonzero of n_p (-1: none)
-    const real wfull = tri_fwd_lds<L>(tid, np_me, Lc, zero, dinv, xs, nf, s0 > 0 ? (s0 & ~(W == 1 ? 3 : kRing2 - 1)) : 0);
+    const real wfull = tri_fwd_lds<L>(np_me, Lc, zero, dinv, xs, nf, s0 > 0 ? (s0 & ~(W == 1 ? 3 : kRing2 - 1)) : 0);
     const real wnorm2 = B::sum(wfull * wfull, red);
     HMPC_TOC(10, t_fwd);
 
@@ -1476,7 +1470,7 @@ __device__ __forceinline__ void solve_instance(const SolveArgs& a, int64_t b, re
       HMPC_TOC(11, t_gs);
       // primal direction z = L^-T w_perp (lane v gets z_v)
       HMPC_TIC(t_bwd);
-      const real zi = tri_bwd<L>(tid, wp, Lc, zero, dinv, xs, nf);
+      const real zi = tri_bwd<L>(wp, Lc, zero, dinv, xs, nf);
       HMPC_TOC(12, t_bwd);
       HMPC_TIC(t_dual);
       // dual direction r = R^-1 c (lanes l < q), back substitution
@@ -1597,12 +1591,12 @@ __device__ __forceinline__ void solve_instance(const SolveArgs& a, int64_t b, re
 #endif
     if (uni(status) != ST_SOLVED && a.ovf_count) status = ST_OVERFLOW;
     if (uni(status) == ST_SOLVED) {
-      const SolveArgs& a = opaque_args(a_);
+      const SolveArgs& ka = opaque_args(a);   // (fresh loads of the arguments)
       double* d64 = reinterpret_cast<double*>(sm + L::R64);
       double* dlo = reinterpret_cast<double*>(sm + L::R64LO);
       int* dslot = reinterpret_cast<int*>(d64 + L::DSLOT);
-      const double dt64 = a.dt, dtm64 = a.dt / a.m;
-      const double mu64 = a.mu ? a.mu[b] : a.mu_default;
+      const double dt64 = ka.dt, dtm64 = ka.dt / ka.m;
+      const double mu64 = ka.mu ? ka.mu[b] : ka.mu_default;
       const double zc64 = dt64 * dtm64;
       const double* xrf7 = reinterpret_cast<const double* const*>(sm + L::XRV)[0];
       const int xrs = reinterpret_cast<const int*>(sm + L::XRV + 2)[0];
@@ -1610,17 +1604,17 @@ __device__ __forceinline__ void solve_instance(const SolveArgs& a, int64_t b, re
       // rows as phase 0 builds them from the fp64 inputs
       if (tid < N) {
         const int k = tid;
-        const double* xp = a.x_lin + b * 12 * (N + 1);
-        const int mode = a.shift_mode;
+        const double* xp = ka.x_lin + b * 12 * (N + 1);
+        const int mode = ka.shift_mode;
         auto xl = [&](int c) -> double {
           if (mode == 0) return xp[12 * k + c];
-          if (k == 0) return a.x_in[b * 12 + c];
+          if (k == 0) return ka.x_in[b * 12 + c];
           return mode == 1 ? xrf7[(k - 1) * xrs + c] : xp[12 * (k + 1 <= N ? k + 1 : N) + c];
         };
         const double p3[3] = {xl(0), xl(1), xl(2)};
-        const double* pfp = a.pf + b * a.pf_bs + k * a.pf_rs;
+        const double* pfp = ka.pf + b * ka.pf_bs + k * ka.pf_rs;
         const double pf3[3] = {pfp[0], pfp[1], pfp[2]};
-        stage_dynamics_vals<VAR, double>(k, xl(5), p3, pf3, a.Jinv, a.rh, dt64, dlo + L::DCS, d64 + L::DBW);
+        stage_dynamics_vals<VAR, double>(k, xl(5), p3, pf3, ka.Jinv, ka.rh, dt64, dlo + L::DCS, d64 + L::DBW);
       }
       // u in full order (fixed variables 0), each lane's full-order slot
       for (int i = tid; i < L::NVF; i += NT) dlo[L::DU + i] = 0.0;
@@ -1629,7 +1623,7 @@ __device__ __forceinline__ void solve_instance(const SolveArgs& a, int64_t b, re
         const int r = i / 12;
         d64[L::DXR + i] = xrf7[r * xrs + i - 12 * r];
       }
-      const double xin64 = a.x_in[b * 12 + (tid < 12 ? tid : 0)];
+      const double xin64 = ka.x_in[b * 12 + (tid < 12 ? tid : 0)];
       B::sync();
       double u64 = (double)v;
       if (active_lane) dlo[L::DU + fidx] = u64;
@@ -1638,8 +1632,8 @@ __device__ __forceinline__ void solve_instance(const SolveArgs& a, int64_t b, re
       const double qr = qdiag(tid);
       const int rw = (tid >= 9 && tid < 12) ? tid - 9 : 0;
       const int rv = (tid >= 6 && tid < 9) ? tid - 6 : 0;
-      const double gdt = tid == 8 ? -a.g * dt64 : 0.0;
-      const double u2mg = 2.0 * a.m * a.g;
+      const double gdt = tid == 8 ? -ka.g * dt64 : 0.0;
+      const double u2mg = 2.0 * ka.m * ka.g;
       const double ub_alias = (sm[L::CC + N - 1] != 0.0) ? u2mg : 0.0;
       B::sync();
       double dg[N];   // W_k (x_{k+1} - r_k) on lanes < 12
@@ -1678,7 +1672,7 @@ __device__ __forceinline__ void solve_instance(const SolveArgs& a, int64_t b, re
           if constexpr (OUT) {
             objl = fma(kf * qr * e, e, objl);
             if constexpr (k < N - 1) {
-              const double ub = a.uref_aliased ? ub_alias : ((sm[L::CC + k] != 0.0) ? u2mg : 0.0);
+              const double ub = ka.uref_aliased ? ub_alias : ((sm[L::CC + k] != 0.0) ? u2mg : 0.0);
               const double du = uk[tu] - (tid == 2 ? ub : 0.0);
               objl = fma(rdu * du, du, objl);
             }
@@ -1711,7 +1705,7 @@ __device__ __forceinline__ void solve_instance(const SolveArgs& a, int64_t b, re
         return sl == 0 ? fma(mu64, fz, -uo) : fma(mu64, fz, uo);
       };
       double objl = 0.0;
-      const int nref = a.refine;
+      const int nref = ka.refine;
 #pragma unroll 1
       for (int it = 0; it < nref; ++it) {
         rollout(std::false_type{}, nullptr, objl);
@@ -1737,7 +1731,7 @@ __device__ __forceinline__ void solve_instance(const SolveArgs& a, int64_t b, re
           for (int r = 0; r < 3; ++r) hacc = fma(vc < 3 ? bv<VAR>(r, vc, dtm64, cpi, spi) : 0.0, aj[r], hacc);
 #pragma unroll
           for (int r = 0; r < 3; ++r) hacc = fma(bwi[6 * r + vc], aj[3 + r], hacc);
-          const double ub = vc == 2 ? (a.uref_aliased ? ub_alias : ((sm[L::CC + vj] != 0.0) ? u2mg : 0.0)) : 0.0;
+          const double ub = vc == 2 ? (ka.uref_aliased ? ub_alias : ((sm[L::CC + vj] != 0.0) ? u2mg : 0.0)) : 0.0;
           const double Vj = (vj == N - 1) ? 0.0 : kRdiag;
           r1 = -2.0 * fma(Vj, u64 - ub, hacc);
         }
@@ -1746,7 +1740,7 @@ __device__ __forceinline__ void solve_instance(const SolveArgs& a, int64_t b, re
         // r2 = b_A - N_A' u (lane l < q: active row l)
         const double r2 = tid < qu ? -slack64(act[tid < qu ? tid : 0]) : 0.0;
         // the correction, on the fp32 factors
-        real w = tri_fwd_lds<L>(tid, (real)r1, Lc, zero, dinv, xs, nf, 0);
+        real w = tri_fwd_lds<L>((real)r1, Lc, zero, dinv, xs, nf, 0);
         real cvec = 0;
         ladder<0, QMAX>(qu, [&](auto lc) __attribute__((always_inline)) {
           constexpr int l = decltype(lc)::value;
@@ -1774,7 +1768,7 @@ __device__ __forceinline__ void solve_instance(const SolveArgs& a, int64_t b, re
           constexpr int l = decltype(lc)::value;
           zq = fma((real)rdlane(tmine, l), Qw[l], zq);
         });
-        const real du = tri_bwd<L>(tid, zq, Lc, zero, dinv, xs, nf);
+        const real du = tri_bwd<L>(zq, Lc, zero, dinv, xs, nf);
         u64 += active_lane ? (double)du : 0.0;
         lam += dlam;
         if (active_lane) dlo[L::DU + fidx] = u64;
@@ -1800,17 +1794,17 @@ __device__ __forceinline__ void solve_instance(const SolveArgs& a, int64_t b, re
       }
       const bool bad = __ballot(worst < -kRefineTol || (tid < qu && lam < -kRefineTol)) != 0;
       if (bad) {
-        status = a.ovf_count ? ST_OVERFLOW : ST_NUMERICAL;
+        status = ka.ovf_count ? ST_OVERFLOW : ST_NUMERICAL;
       } else {
         B::sync();
-        if (tid < L::NVF) a.u[b * L::NVF + tid] = dlo[L::DU + tid];
-        if (a.x)
-          for (int i = tid; i < 12 * (N + 1); i += NT) a.x[b * 12 * (N + 1) + i] = xo[i];
+        if (tid < L::NVF) ka.u[b * L::NVF + tid] = dlo[L::DU + tid];
+        if (ka.x)
+          for (int i = tid; i < 12 * (N + 1); i += NT) ka.x[b * 12 * (N + 1) + i] = xo[i];
         if (tid == 0) {
-          if (a.obj) a.obj[b] = objv;
-          a.status[b] = ST_SOLVED;
-          if (a.iters) a.iters[b] = iters;
-          if (a.active) a.active[b] = q;
+          if (ka.obj) ka.obj[b] = objv;
+          ka.status[b] = ST_SOLVED;
+          if (ka.iters) ka.iters[b] = iters;
+          if (ka.active) ka.active[b] = q;
         }
         return;
       }
@@ -1881,7 +1875,7 @@ __device__ __forceinline__ void solve_instance(const SolveArgs& a, int64_t b, re
         bv_u = (rv == 0) ? dtm2 * (cp * u0 - sp * u1) : ((rv == 1) ? dtm2 * (sp * u0 + cp * u1) : dtm2 * u2);
       }
       const real bu = (tid >= 9 && tid < 12) ? bw_u : ((tid >= 6 && tid < 9) ? bv_u : 0.0);
-      xr = ad_lane(xr, dt, cp, sp, tid) + bu + gdt;
+      xr = ad_lane(xr, dt, cp, sp) + bu + gdt;
       const real kf = (k == N - 1) ? kTermQ : 1.0;
       const real e = xr - xrg[k];
       objl = fma(kf * qr * e, e, objl);
@@ -1913,69 +1907,20 @@ __device__ __forceinline__ void solve_instance(const SolveArgs& a, int64_t b, re
   }
 }
 
-// One instance per workgroup: block i solves instance i, or (split launch)
-// the i-th instance of its class list; blocks beyond the list have no work.
-template <int VAR, int N, typename R, int NVM = 0, int QM = 0>
-__global__ void __launch_bounds__((Lay<N, NVM, QM>::NT), (waves_of<N, NVM, QM>()))
-solve_kernel(SolveArgs a) {
-  static_assert(sizeof(R) == sizeof(real), "one arithmetic type per build");
-  __shared__ __attribute__((aligned(16))) real sm[Lay<N, NVM, QM>::TOTAL];
-  int64_t b = blockIdx.x;
-  if (a.list) {
-    if ((int)blockIdx.x >= *a.list_count) return;
-    b = a.list[blockIdx.x];
-  }
-  solve_instance<VAR, N, NVM, QM>(a, b, sm, (int)threadIdx.x);
-}
-// Persistent form of a split class (one wave per workgroup, a resident grid):
-// each workgroup takes the next entry of its class list off the class's
-// counter (a.list_work, zero at the launch; the overflow pass zeroes it at
-// its end) until the list is done.
-template <int VAR, int N, typename R, int NVM, int QM>
-__global__ void __launch_bounds__(64, (waves_of<N, NVM, QM>()))
-solve_kernel_p(SolveArgs a) {
-  static_assert(sizeof(R) == sizeof(real), "one arithmetic type per build");
-  static_assert(Lay<N, NVM, QM>::W == 1, "persistent classes are one wave");
-  __shared__ __attribute__((aligned(16))) real sm[Lay<N, NVM, QM>::TOTAL];
-  const int n = *a.list_count;
-  while (true) {
-    int i = 0;
-    if (threadIdx.x == 0) i = atomicAdd(a.list_work, 1);
-    i = __builtin_amdgcn_readfirstlane(i);
-    if (i >= n) break;
-    // lane and the argument block through volatile asm, afresh for every
-    // instance: nothing derived from them (lane masks, addresses, constants
-    // from dt / m / g) is hoisted out of this loop and held for its life
-    int tid;
-    asm volatile("v_mov_b32 %0, %1" : "=v"(tid) : "v"((int)threadIdx.x));
-#ifdef __HIP_DEVICE_COMPILE__   // (the host pass only parses this body)
-    typedef const __attribute__((address_space(4))) SolveArgs karg_t;
-    karg_t* ap = (karg_t*)__builtin_amdgcn_kernarg_segment_ptr();
-    asm volatile("" : "+s"(ap));
-    const SolveArgs ai = *ap;
-#else
-    const SolveArgs& ai = a;
-#endif
-    solve_instance<VAR, N, NVM, QM>(ai, a.list[i], sm, tid);
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-  }
-}
-
-// Split launch: each instance goes to one of up to three classes by its free
-// variables nf = 3N + (3f: 3, 2f: 2) x stance stages (the number of stance
-// stages of its contact schedule C): the narrow class (nf <= NVS, NVS > 0),
-// the compacted class (nf <= NVM) or the full class.  One thread per
-// instance; the class lists are appended block by block (one atomic per block
-// and list): list 0 (compacted) at split_list[0..B), list 1 (full) at
-// [B..2B), list 2 (narrow) at [2B..3B), lengths in split_count[0..2] (zero at
-// the launch; the overflow pass zeroes them).
+// Split launch: each instance goes to the compacted one-wave kernel (at most
+// NVM free variables: NVM-wide rows, 3 waves / SIMD) or to the full kernel,
+// by the number of stance stages of its contact schedule C (free variables
+// nf = 3N + (3f: 3, 2f: 2) x stance stages).  One thread per instance; the
+// two class lists are appended block by block (one atomic per block and list):
+// list A at split_list[0..B), list B at split_list[B..2B), lengths in
+// split_count[0..1] (zero at the launch; the overflow pass zeroes them).
 constexpr int kClsT = 1024;   // classify threads per block
-template <int VAR, int N, int NVM, int NVS>
+template <int VAR, int N, int NVM>
 __global__ void __launch_bounds__(kClsT) classify_kernel(SolveArgs a) {
-  // (one atomic per block and list: per-wave atomics on the counters
+  // (one atomic per block and list: per-wave atomics on the two counters
   // serialised at the L2 and made this pass 25 us of a 1.3 ms step)
-  __shared__ int wc[kClsT / 64][3];
-  __shared__ int base[3];
+  __shared__ int wc[kClsT / 64][2];
+  __shared__ int base[2];
   const int64_t i = (int64_t)blockIdx.x * kClsT + threadIdx.x;
   const bool in = i < a.B;
   int nst = 0;
@@ -1985,61 +1930,30 @@ __global__ void __launch_bounds__(kClsT) classify_kernel(SolveArgs a) {
     for (int k = 0; k < N; ++k) nst += c[k] != 0.0 ? 1 : 0;
   }
   const int nf = 3 * N + (VAR == 3 ? 3 : 2) * nst;
-  const int cls = !in ? -1 : (nf <= NVS ? 2 : (nf <= NVM ? 0 : 1));
-  uint64_t m[3];
-#pragma unroll
-  for (int l = 0; l < 3; ++l) m[l] = __ballot(cls == l);
+  const bool cmp = in && nf <= NVM, full = in && !cmp;
+  const uint64_t mc = __ballot(cmp), mf = __ballot(full);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  if (lane == 0)
-#pragma unroll
-    for (int l = 0; l < 3; ++l) wc[w][l] = __builtin_popcountll(m[l]);
+  if (lane == 0) {
+    wc[w][0] = __builtin_popcountll(mc);
+    wc[w][1] = __builtin_popcountll(mf);
+  }
   __syncthreads();
   if (threadIdx.x == 0) {   // exclusive scan of the wave counts, one atomic per list
-    int t[3] = {0, 0, 0};
-    for (int v = 0; v < kClsT / 64; ++v)
-#pragma unroll
-      for (int l = 0; l < 3; ++l) {
-        const int c = wc[v][l];
-        wc[v][l] = t[l];
-        t[l] += c;
-      }
-#pragma unroll
-    for (int l = 0; l < 3; ++l) base[l] = t[l] ? atomicAdd(a.split_count + l, t[l]) : 0;
+    int tc = 0, tf = 0;
+    for (int v = 0; v < kClsT / 64; ++v) {
+      const int c = wc[v][0], f = wc[v][1];
+      wc[v][0] = tc;
+      wc[v][1] = tf;
+      tc += c;
+      tf += f;
+    }
+    base[0] = tc ? atomicAdd(a.split_count, tc) : 0;
+    base[1] = tf ? atomicAdd(a.split_count + 1, tf) : 0;
   }
   __syncthreads();
-  if (cls >= 0) {
-    const uint64_t lt = (1ull << lane) - 1;
-    a.split_list[cls * a.B + base[cls] + wc[w][cls] + __builtin_popcountll(m[cls] & lt)] = (int32_t)i;
-  }
-}
-
-// resident workgroups of a persistent class kernel (occupancy x CUs, queried
-// once per process)
-template <typename K>
-unsigned persistent_grid(K kern, unsigned bs) {
-  int dev = 0, cus = 0, per = 0;
-  if (hipGetDevice(&dev) != hipSuccess ||
-      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void*>(kern), (int)bs, 0) != hipSuccess ||
-      per < 1 || cus < 1)
-    return 0;
-  return (unsigned)(per * cus);
-}
-// a class's launch: one workgroup per batch entry (blocks past the list exit)
-template <typename K>
-bool launch_grid(K kern, const SolveArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(kern, dim3((unsigned)a.B), dim3(64), 0, s, a);
-  return true;
-}
-// ... or the persistent kernel over its list (grid = the resident
-// workgroups, capped at the batch)
-template <typename K>
-bool launch_class(K kern, const SolveArgs& a, hipStream_t s) {
-  static const unsigned g = persistent_grid(kern, 64);
-  if (g == 0) return false;
-  const unsigned grid = (int64_t)g < a.B ? g : (unsigned)a.B;
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(64), 0, s, a);
-  return true;
+  const uint64_t lt = (1ull << lane) - 1;
+  if (cmp) a.split_list[base[0] + wc[w][0] + __builtin_popcountll(mc & lt)] = (int32_t)i;
+  if (full) a.split_list[a.B + base[1] + wc[w][1] + __builtin_popcountll(mf & lt)] = (int32_t)i;
 }
 
 }  // namespace
@@ -2058,31 +1972,10 @@ bool launch_class(K kern, const SolveArgs& a, hipStream_t s) {
 #ifndef HMPC_LAUNCH_SUFFIX
 #define HMPC_LAUNCH_SUFFIX
 #endif
-// Split-class kernels: persistent (solve_kernel_p over the class list, a
-// resident grid; default) or one workgroup per batch entry (solve_kernel,
-// blocks past the list's length exit).  HMPC_SPLIT_PERSIST=0 builds the
-// latter (A/B).
-#ifndef HMPC_SPLIT_PERSIST
-#define HMPC_SPLIT_PERSIST 0
-#endif
-// 1: the full class on the high-priority split stream, the compacted one on
-// the caller's; 0: the full class on the caller's stream, the compacted one on
-// a split stream of the same priority (hmpc_capi.cpp creates them)
-#ifndef HMPC_SPLIT_PRIO
-#define HMPC_SPLIT_PRIO 0
-#endif
-#if HMPC_SPLIT_PERSIST
-#define HMPC_CLASS_LAUNCH(...) launch_class(solve_kernel_p<__VA_ARGS__>, a, s)
-#else
-#define HMPC_CLASS_LAUNCH(...) launch_grid(solve_kernel<__VA_ARGS__>, a, s)
-#endif
 #if defined(HMPC_CMP_NV) && HMPC_CMP_NV > 0
-// the split's compacted (and narrow) kernels launch from a translation unit
-// of their own (-DHMPC_CMP_ONLY): the objects build in parallel
+// the split's compacted kernel launches from a translation unit of its own
+// (-DHMPC_CMP_ONLY): the objects build in parallel
 bool HMPC_CAT(launch_cmp_n, HMPC_INST_N)(int variant, const SolveArgs& a, hipStream_t s);
-#if HMPC_SML_NV > 0
-bool HMPC_CAT(launch_sml_n, HMPC_INST_N)(int variant, const SolveArgs& a, hipStream_t s);
-#endif
 // 2f's full class: at most 5N free variables (3N torques + 2N stance forces;
 // f_y is fixed), so a 5N-wide compacted kernel replaces the 6N-wide full one
 // when 5N rows fit one wave (same capacity as the full kernel)
@@ -2094,35 +1987,20 @@ bool HMPC_CAT(launch_full2f_n, HMPC_INST_N)(const SolveArgs& a, hipStream_t s);
 #endif
 #ifdef HMPC_CMP_ONLY
 bool HMPC_CAT(launch_cmp_n, HMPC_INST_N)(int variant, const SolveArgs& a, hipStream_t s) {
-  if (variant == 3) return HMPC_CLASS_LAUNCH(3, HMPC_INST_N, real, HMPC_CMP_NV, HMPC_CMP_Q);
-  return HMPC_CLASS_LAUNCH(2, HMPC_INST_N, real, HMPC_CMP_NV, HMPC_CMP_Q);
+  if (variant == 3)
+    hipLaunchKernelGGL((solve_kernel<3, HMPC_INST_N, real, HMPC_CMP_NV, HMPC_CMP_Q>), dim3((unsigned)a.B), dim3(64), 0, s, a);
+  else
+    hipLaunchKernelGGL((solve_kernel<2, HMPC_INST_N, real, HMPC_CMP_NV, HMPC_CMP_Q>), dim3((unsigned)a.B), dim3(64), 0, s, a);
+  return true;
 }
-#if HMPC_SML_NV > 0
-bool HMPC_CAT(launch_sml_n, HMPC_INST_N)(int variant, const SolveArgs& a, hipStream_t s) {
-  if (variant == 3) return HMPC_CLASS_LAUNCH(3, HMPC_INST_N, real, HMPC_SML_NV, HMPC_CMP_Q);
-  return HMPC_CLASS_LAUNCH(2, HMPC_INST_N, real, HMPC_SML_NV, HMPC_CMP_Q);
-}
-#endif
 #ifdef HMPC_FULL2F_NV
 bool HMPC_CAT(launch_full2f_n, HMPC_INST_N)(const SolveArgs& a, hipStream_t s) {
-  return HMPC_CLASS_LAUNCH(2, HMPC_INST_N, real, HMPC_FULL2F_NV, HMPC_FULL2F_Q);
+  hipLaunchKernelGGL((solve_kernel<2, HMPC_INST_N, real, HMPC_FULL2F_NV, HMPC_FULL2F_Q>), dim3((unsigned)a.B), dim3(64), 0,
+                     s, a);
+  return true;
 }
 #endif
 #else
-namespace {
-#if defined(HMPC_CMP_NV) && HMPC_CMP_NV > 0
-bool launch_full3f(const SolveArgs& a, hipStream_t s) { return HMPC_CLASS_LAUNCH(3, HMPC_INST_N, real, 0, 0); }
-// a class on stream t, forked from s after the classify pass (fork event
-// recorded on s) and joined back into s by `join`
-template <typename F>
-bool on_stream(hipStream_t s, hipStream_t t, hipEvent_t fork, hipEvent_t join, F&& launch) {
-  if (t == nullptr || t == s) return launch(s);
-  if (hipStreamWaitEvent(t, fork, 0) != hipSuccess) return false;
-  if (!launch(t)) return false;
-  return hipEventRecord(join, t) == hipSuccess && hipStreamWaitEvent(s, join, 0) == hipSuccess;
-}
-#endif
-}  // namespace
 bool HMPC_CAT(HMPC_CAT(launch_solve_n, HMPC_INST_N), HMPC_LAUNCH_SUFFIX)(int variant, const SolveArgs& a,
                                                                      hipStream_t s) {
   constexpr int N = HMPC_INST_N;
@@ -2132,53 +2010,36 @@ bool HMPC_CAT(HMPC_CAT(launch_solve_n, HMPC_INST_N), HMPC_LAUNCH_SUFFIX)(int var
   SolveArgs af = a;
   af.list = nullptr;
   af.list_count = nullptr;
-  af.list_work = nullptr;
 #if defined(HMPC_CMP_NV) && HMPC_CMP_NV > 0
   if (a.split_list && a.split_count) {   // classify, then one launch per class
     const unsigned cb = (unsigned)((a.B + kClsT - 1) / kClsT);
-    auto cls = [&](int l) {   // the args of class list l
-      SolveArgs c = af;
-      c.list = a.split_list + l * a.B;
-      c.list_count = a.split_count + l;
-      c.list_work = a.split_count + 3 + l;
-      return c;
-    };
-    const SolveArgs ac = cls(0), afl = cls(1);
-    if (variant == 3) hipLaunchKernelGGL((classify_kernel<3, N, HMPC_CMP_NV, HMPC_SML_NV>), dim3(cb), dim3(kClsT), 0, s, a);
-    else hipLaunchKernelGGL((classify_kernel<2, N, HMPC_CMP_NV, HMPC_SML_NV>), dim3(cb), dim3(kClsT), 0, s, a);
-    // the classes run concurrently: the full class on the high-priority
-    // split stream (its waves take the SIMDs first: the longest instances,
-    // 2 waves / SIMD), the compacted one on the caller's stream (3 waves /
-    // SIMD once the full waves are done), the narrow one on the low-priority
-    // split stream; joined back into the caller's stream before the overflow
-    // pass
-    const bool fork = a.split_fork && (a.split_stream[0] || a.split_stream[1]);
-    if (fork && hipEventRecord(a.split_fork, s) != hipSuccess) return false;
-    hipStream_t t0 = fork ? a.split_stream[0] : s, t1 = fork ? a.split_stream[1] : s;
-    auto full = [&](hipStream_t t) {
-      return variant == 3 ? launch_full3f(afl, t)
+    SolveArgs ac = af;
+    ac.list = a.split_list;
+    ac.list_count = a.split_count;
+    af.list = a.split_list + a.B;
+    af.list_count = a.split_count + 1;
+    if (variant == 3) hipLaunchKernelGGL((classify_kernel<3, N, HMPC_CMP_NV>), dim3(cb), dim3(kClsT), 0, s, a);
+    else hipLaunchKernelGGL((classify_kernel<2, N, HMPC_CMP_NV>), dim3(cb), dim3(kClsT), 0, s, a);
+    // the two classes run concurrently: the full kernel on the caller's
+    // stream, the compacted one on the split stream, joined back before the
+    // overflow pass (one kernel's tail fills with the other's waves)
+    hipStream_t s2 = s;
+    if (a.split_stream && a.split_fork && a.split_join) {
+      if (hipEventRecord(a.split_fork, s) != hipSuccess) return false;
+      if (hipStreamWaitEvent(a.split_stream, a.split_fork, 0) != hipSuccess) return false;
+      s2 = a.split_stream;
+    }
+    if (variant == 3) hipLaunchKernelGGL((solve_kernel<3, N, real>), dim3((unsigned)a.B), dim3(NT), 0, s, af);
 #ifdef HMPC_FULL2F_NV
-                          : HMPC_CAT(launch_full2f_n, HMPC_INST_N)(afl, t);
+    else HMPC_CAT(launch_full2f_n, HMPC_INST_N)(af, s);
 #else
-                          : (hipLaunchKernelGGL((solve_kernel<2, N, real>), dim3((unsigned)a.B), dim3(NT), 0, t, afl), true);
+    else hipLaunchKernelGGL((solve_kernel<2, N, real>), dim3((unsigned)a.B), dim3(NT), 0, s, af);
 #endif
-    };
-    auto cmp = [&](hipStream_t t) { return HMPC_CAT(launch_cmp_n, HMPC_INST_N)(variant, ac, t); };
-#if HMPC_SPLIT_PRIO
-    if (!on_stream(s, t0, a.split_fork, a.split_join[0], full)) return false;
-    if (!cmp(s)) return false;
-#else   // the full class on the caller's stream, the compacted one forked (same priority)
-    if (!full(s)) return false;
-    if (!on_stream(s, t0, a.split_fork, a.split_join[0], cmp)) return false;
-#endif
-#if HMPC_SML_NV > 0
-    const SolveArgs asm_ = cls(2);
-    if (!on_stream(s, t1, a.split_fork, a.split_join[1],
-                   [&](hipStream_t t) { return HMPC_CAT(launch_sml_n, HMPC_INST_N)(variant, asm_, t); }))
-      return false;
-#else
-    (void)t1;
-#endif
+    HMPC_CAT(launch_cmp_n, HMPC_INST_N)(variant, ac, s2);
+    if (s2 != s) {
+      if (hipEventRecord(a.split_join, s2) != hipSuccess) return false;
+      if (hipStreamWaitEvent(s, a.split_join, 0) != hipSuccess) return false;
+    }
     return true;
   }
 #endif
@@ -2218,16 +2079,12 @@ const char* HMPC_CAT(HMPC_CAT(name_solve_n, HMPC_INST_N), HMPC_LAUNCH_SUFFIX)(in
       name += buf;
     };
 #if defined(HMPC_CMP_NV) && HMPC_CMP_NV > 0
-    const char* k = HMPC_SPLIT_PERSIST ? "solve_kernel_p" : "solve_kernel";
-#if HMPC_SML_NV > 0
-    add(k, HMPC_SML_NV, HMPC_CMP_Q);
-#endif
-    add(k, HMPC_CMP_NV, HMPC_CMP_Q);
+    add("solve_kernel", HMPC_CMP_NV, HMPC_CMP_Q);
 #ifdef HMPC_FULL2F_NV
-    if (variant == 2) add(k, HMPC_FULL2F_NV, HMPC_FULL2F_Q);
-    else add(k, 0, 0);
+    if (variant == 2) add("solve_kernel", HMPC_FULL2F_NV, HMPC_FULL2F_Q);
+    else add("solve_kernel", 0, 0);
 #else
-    add(variant == 3 ? k : "solve_kernel", 0, 0);
+    add("solve_kernel", 0, 0);
 #endif
 #else
     add("solve_kernel", 0, 0);

@@ -1435,7 +1435,7 @@ __global__ void __launch_bounds__(RT) ric_overflow_kernel(SolveArgs a, int N) {
     __syncthreads();
   }
   // the last workgroup out zeroes [overflow count | instance counter | its
-  // own done counter | the dense split's counts and claim counters] for the next solve on this stream (every group read
+  // own done counter | the dense split's counts] for the next solve on this stream (every group read
   // the count above before it counts itself done): no memset per solve
   if (threadIdx.x == 0) {
     __threadfence();
@@ -1443,7 +1443,8 @@ __global__ void __launch_bounds__(RT) ric_overflow_kernel(SolveArgs a, int N) {
       atomicExch(a.ovf_count, 0);
       atomicExch(a.ovf_count + 1, 0);
       atomicExch(a.ovf_count + 2, 0);
-      for (int i = 3; i < 9; ++i) atomicExch(a.ovf_count + i, 0);   // the dense split's class counts, claims
+      atomicExch(a.ovf_count + 3, 0);   // the dense split's class counts
+      atomicExch(a.ovf_count + 4, 0);
     }
   }
 }
