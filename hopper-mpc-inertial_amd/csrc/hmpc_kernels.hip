@@ -1109,7 +1109,7 @@ solve_kernel(SolveArgs a) {
         constexpr int NCH = (NV - JA + CW - 1) / CW;
         constexpr int NAHEAD = (k + 1 < NV) ? 1 + nldc((k + 2) & ~1, 0) : 0;   // LDS ops of ahead()
         const real rs = p_rs, tk = p_tk;
-        lds_wait<0>(nb[0], nb[1]);   // this step's chunk 0 (and everything older)
+        if constexpr (k == 0) lds_wait<0>(nb[0], nb[1]);   // chunk 0 (later steps: waited at the previous one's end)
         // every lane updates: a lane <= k changes only its registers > k, the
         // upper triangle of its row (don't-care, overwritten at their step)
         const real nt = -tk;
@@ -1173,16 +1173,14 @@ solve_kernel(SolveArgs a) {
           lds_wait<younger>(buf[ch % 3][0], buf[ch % 3][1]);
           update(chc, buf[ch % 3]);
         });
-        // the last step (k + 1 == nf) looked ahead into a padding column:
-        // drain that load here, before the ladder's exit branch, so no LDS
-        // load is in flight where the exits merge (the compiler may copy or
-        // reassign nb's registers at a merge; a variant that let it do so
-        // returned wrong optima)
-        if constexpr (k + 1 < NV) {
-          if (k + 1 >= nf) lds_wait<0>(nb[0], nb[1]);
-        }
+        // the next step's chunk 0 (the lookahead) is waited for here, at the
+        // end of this step rather than at the start of the next: the same
+        // wait point, but before the ladder's exit test, so no LDS load is in
+        // flight where an early exit (nf < NV) merges with the others (the
+        // compiler may copy or reassign nb's registers at a merge; a variant
+        // that let it do so returned wrong optima)
+        if constexpr (k + 1 < NV) lds_wait<0>(nb[0], nb[1]);
       });
-      lds_wait<0>(nb[0], nb[1]);   // (nothing in flight: a no-op wait)
     } else {
       real mine = Rg[0];   // A[tid][k] of the current step
       // pivot extras (diag_extra) by lane, behind the column buffers (the
@@ -1966,6 +1964,7 @@ __global__ void __launch_bounds__(kClsT) classify_kernel(SolveArgs a) {
 #ifndef HMPC_INST_N
 #error "compile with -DHMPC_INST_N=<horizon>"
 #endif
+
 #define HMPC_CAT2(a, b) a##b
 #define HMPC_CAT(a, b) HMPC_CAT2(a, b)
 

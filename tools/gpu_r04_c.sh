@@ -13,3 +13,7 @@ for k in 4 5 6; do
   timeout -k 10 300 python bench.py --precision f32_refined --refine $k --cpu-seconds 4 > gpurun_out/r04c_f32r_k$k.json 2> gpurun_out/r04c_f32r_k$k.err; rc=$?; stop $rc
   python -c "import json; d=json.load(open('gpurun_out/r04c_f32r_k$k.json')); print('f32r k=$k', round(d['value']/1e6,3), 'M/s du', d['parity_sample']['max_abs_du_vs_port'], d['parity_sample']['status_mismatch'])"
 done
+timeout -k 10 600 python tools/ab.py --tag r04c_cfg2 --rounds 2 libhmpc.so libhmpc_filt.so || exit 1
+timeout -k 10 600 python tools/ab.py --tag r04c_cfg1 --rounds 2 --args "--variant 2f --straight --batch 4096" libhmpc.so libhmpc_filt.so || exit 1
+timeout -k 10 900 python tools/ab.py --tag r04c_cfg3 --rounds 2 --args "--N 20 --straight --mu-sweep --global-batch 262144 --steps 10 --warmup 3" libhmpc.so libhmpc_ricold.so || exit 1
+timeout -k 10 600 python tools/ab.py --tag r04c_n60 --rounds 2 --args "--N 60 --straight --batch 4096 --steps 10 --warmup 3" libhmpc.so libhmpc_ricold.so || exit 1
