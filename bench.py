@@ -121,7 +121,7 @@ def parse():
                     help='f64 = the fastest fp64 kernel for N (default); f32 = fp32 one-wave '
                          'kernel, f32_refined = fp32 + --refine fp64 corrections (configs[4]); '
                          'others force a kernel for A/B runs')
-    ap.add_argument('--refine', type=int, default=2, help='fp64 corrections of f32_refined')
+    ap.add_argument('--refine', type=int, default=5, help='fp64 corrections of f32_refined (5: max|du| <= 1e-6)')
     ap.add_argument('--cpu-seconds', type=float, default=12.0,
                     help='budget of the bounded CPU-baseline sample, split over its two legs '
                          '(all cores, then one core); 0 disables')

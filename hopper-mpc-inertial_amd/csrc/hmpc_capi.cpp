@@ -25,7 +25,7 @@ struct hmpc_ctx {
   double rh[3];
   int uref_mode;
   int precision = HMPC_PREC_F64;
-  int refine = 2;   // fp64 corrections of HMPC_PREC_F32_REFINED (hmpc_set_refinement)
+  int refine = 5;   // fp64 corrections of HMPC_PREC_F32_REFINED (hmpc_set_refinement)
   std::string err;
   // staging buffers (host API) and mpcontrol scratch
   void* dbuf = nullptr;

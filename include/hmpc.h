@@ -238,8 +238,10 @@ int hmpc_gait_batch(hmpc_ctx* ctx, int n_steps, int mpc_factor, int N, double dt
    (reduced Hessian condition ~3e6), see DESIGN.md. */
 int hmpc_set_precision(hmpc_ctx* ctx, int precision);
 
-/* Number of fp64 corrections HMPC_PREC_F32_REFINED runs (0..16, default 2;
-   each costs an fp64 rollout + adjoint and two fp32 sweeps per instance). */
+/* Number of fp64 corrections HMPC_PREC_F32_REFINED runs (0..16, default 5:
+   each contracts the error by ~cond x eps32, measured max|du| 1.7e-3 / 7.4e-5 /
+   3.1e-6 / 1.3e-7 / 6.4e-9 after 2 / 3 / 4 / 5 / 6 on configs[4]; each costs an
+   fp64 rollout + adjoint and two fp32 sweeps per instance). */
 int hmpc_set_refinement(hmpc_ctx* ctx, int corrections);
 
 /* Name of the solve kernel this context's (variant, N, precision) runs on,

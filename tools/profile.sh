@@ -1,20 +1,21 @@
 #!/bin/bash
-# Round-3 profile evidence, one GPU call: for each configuration a bench line,
+# Profile evidence, one GPU call: for each configuration a bench line,
 # a rocprofv3 --kernel-trace --stats run of the same command and the PMC
 # passes (one rocprofv3 --pmc run per counter group, each under its own time
-# limit).  Outputs gpurun_out/<tag>/<cfg>/; tools/summarize_r03.py copies the
+# limit).  Outputs gpurun_out/<tag>/<cfg>/; tools/summarize.py copies the
 # judged summaries into profiles/.
 set -u
 R=${GRAFT_REPO_ROOT:-$PWD}
-TAG=${1:-r03}
+TAG=${1:-r04}
 shift || true
-CFGS=${CFGS:-"n10 n20 n60 n10_2f n10_f32"}
+CFGS=${CFGS:-"n10 n20 n60 n10_2f n10_f32 n10_f32r"}
 declare -A ARGS=(
   [n10]="--N 10"
   [n20]="--N 20 --straight --mu-sweep --global-batch 262144"
   [n60]="--N 60 --straight --batch 4096"
   [n10_2f]="--variant 2f --N 10 --straight --batch 4096"
   [n10_f32]="--N 10 --precision f32"
+  [n10_f32r]="--N 10 --precision f32_refined --refine 5"
 )
 for cfg in $CFGS; do
   O=$R/gpurun_out/$TAG/$cfg

@@ -1,6 +1,6 @@
-"""Copy the judged profile evidence of tools/profile_r03.sh into profiles/.
+"""Copy the judged profile evidence of tools/profile.sh into profiles/.
 
-    python tools/summarize_r03.py r03 [cfg ...]
+    python tools/summarize.py r04 [cfg ...]
 
 For each configuration (gpurun_out/<tag>/<cfg>/) writes
   profiles/<tag>_<cfg>_bench.json        the bench line of that call
