@@ -36,8 +36,8 @@ struct hmpc_ctx {
   double* wsbuf = nullptr;
   int wsgroups = 0;
   // active-set overflow pass (hmpc_ric.hip): [overflow count | Riccati
-  // instance counter | done counter | split counts (2) | pad (3) | list of
-  // ovf_cap ids] and the global R blocks of its workgroups
+  // instance counter | done counter | split counts (up to N + 1 <= 13
+  // buckets) | list of ovf_cap ids] and the global R blocks of its workgroups
   int32_t* ovf = nullptr;
   int64_t ovf_cap = 0;
   // the counters need a zeroing before the next solve (fresh buffer, or a
@@ -98,6 +98,7 @@ hmpc::SolveArgs make_args(hmpc_ctx* c, int64_t B, const double* x_in, const doub
   a.ovf_count = nullptr; a.ovf_list = nullptr; a.rws = nullptr; a.rws_stride = 0;
   a.work = nullptr; a.kws = nullptr; a.kws_stride = 0; a.ric_groups = 0;
   a.split_count = nullptr; a.split_list = nullptr; a.list = nullptr; a.list_count = nullptr;
+  a.lpt_lo = 0; a.lpt_hi = -1; a.split_nbkt = 0;
   a.split_stream = nullptr; a.split_fork = nullptr; a.split_join = nullptr;
   a.precision = c->precision;
   a.refine = c->refine;
@@ -139,7 +140,7 @@ int prepare_ws(hmpc_ctx* c, int64_t B, hmpc::SolveArgs& a) {
 // active set outgrew the main kernel's capacity.
 constexpr int kOvfGroups = 128;
 // ints before the overflow list in the counter buffer (see hmpc_ctx::ovf)
-constexpr int kOvfHeader = 8;
+constexpr int kOvfHeader = 16;
 
 // Buffers of the dense / Riccati kernels: [overflow count | instance counter |
 // pad | overflow list], the overflow pass's blocks, the Riccati kernel's
@@ -193,12 +194,13 @@ int prepare_ric(hmpc_ctx* c, int64_t B, hmpc::SolveArgs& a) {
   // the dense kernel's split launch (compacted kernel for the instances with
   // few free variables): class counts next to the overflow counters, which
   // the overflow pass zeroes together at its end
-  if (k == hmpc::Kernel::Dense && hmpc::dense_split_nv(c->N, 0) > 0) {
+  if (k == hmpc::Kernel::Dense && hmpc::dense_split_nv(c->N, 0) > 0 && c->N + 1 <= kOvfHeader - 3) {
     if (B > c->split_cap) {
       if (c->split) (void)hipFree(c->split);
       c->split = nullptr;
       c->split_cap = 0;
-      hipError_t e = hipMalloc(&c->split, sizeof(int32_t) * 2 * (size_t)B);
+      // (up to N + 1 stance-count buckets of B entries, HMPC_SPLIT_LPT)
+      hipError_t e = hipMalloc(&c->split, sizeof(int32_t) * (size_t)(c->N + 1) * (size_t)B);
       if (e != hipSuccess) { c->err = "split list hipMalloc"; return HMPC_ERR_NOMEM; }
       c->split_cap = B;
     }
@@ -212,6 +214,7 @@ int prepare_ric(hmpc_ctx* c, int64_t B, hmpc::SolveArgs& a) {
     }
     a.split_count = c->ovf + 3;
     a.split_list = c->split;
+    a.split_nbkt = c->N + 1;
     a.split_stream = c->split_stream;
     a.split_fork = c->split_fork;
     a.split_join = c->split_join;
@@ -246,7 +249,7 @@ int run_solve(hmpc_ctx* c, hmpc::SolveArgs a, hipStream_t s) {
   // next solve's kernels see them zero).  The CasADi kernel has no overflow
   // pass.
   if (a.work && (!a.ovf_count || c->ovf_dirty)) {
-    hipError_t e = hipMemsetAsync(a.work - 1, 0, (a.ovf_count ? 5 : 3) * sizeof(int32_t), s);
+    hipError_t e = hipMemsetAsync(a.work - 1, 0, (a.ovf_count ? kOvfHeader : 3) * sizeof(int32_t), s);
     if (e != hipSuccess) return fail_hip(c, e, "hipMemsetAsync(overflow count)");
   }
   c->ovf_dirty = true;   // until the overflow pass is launched

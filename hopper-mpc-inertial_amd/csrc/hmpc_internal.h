@@ -72,6 +72,11 @@ struct SolveArgs {
   int32_t* split_list;
   const int32_t* list;
   const int32_t* list_count;
+  // HMPC_SPLIT_LPT builds: the class lists are buckets by stance-stage count
+  // (list[s * B ..], count list_count[s]); a launch serves buckets
+  // lpt_lo..lpt_hi, costliest (most stance stages) first.  lpt_hi < 0: one
+  // plain list.  split_nbkt: the bucket counters the overflow pass zeroes.
+  int lpt_lo, lpt_hi, split_nbkt;
   // the split's second class runs concurrently on split_stream (forked from
   // and joined back into the caller's stream by the two events); nullptr:
   // both classes on the caller's stream, one after the other

@@ -614,8 +614,19 @@ solve_kernel(SolveArgs a) {
   // kernel's class list; blocks beyond the list's length have no work
   int64_t b = blockIdx.x;
   if (a.list) {
-    if ((int)blockIdx.x >= *a.list_count) return;
-    b = a.list[blockIdx.x];
+    if (a.lpt_hi >= 0) {   // stance-count buckets, costliest first (HMPC_SPLIT_LPT)
+      int i = blockIdx.x, s = a.lpt_hi;
+      for (; s >= a.lpt_lo; --s) {
+        const int c = a.list_count[s];
+        if (i < c) break;
+        i -= c;
+      }
+      if (s < a.lpt_lo) return;
+      b = a.list[(int64_t)s * a.B + i];
+    } else {
+      if ((int)blockIdx.x >= *a.list_count) return;
+      b = a.list[blockIdx.x];
+    }
   }
   const real dt = a.dt;
   const real dtm = dt / real(a.m);
@@ -1913,6 +1924,43 @@ solve_kernel(SolveArgs a) {
 // list A at split_list[0..B), list B at split_list[B..2B), lengths in
 // split_count[0..1] (zero at the launch; the overflow pass zeroes them).
 constexpr int kClsT = 1024;   // classify threads per block
+// HMPC_SPLIT_LPT: one list per stance-stage count s = 0..N instead (bucket s
+// at split_list[s B ..), its length in split_count[s]); each class kernel
+// then takes its buckets costliest first (longest-processing-time order).
+template <int VAR, int N>
+__global__ void __launch_bounds__(kClsT) classify_buckets_kernel(SolveArgs a) {
+  __shared__ int wc[kClsT / 64][N + 1];
+  __shared__ int base[N + 1];
+  const int64_t i = (int64_t)blockIdx.x * kClsT + threadIdx.x;
+  const bool in = i < a.B;
+  int nst = 0;
+  if (in) {
+    const double* c = a.C + i * a.C_bs;
+#pragma unroll
+    for (int k = 0; k < N; ++k) nst += c[k] != 0.0 ? 1 : 0;
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint64_t mine = 0;
+#pragma unroll
+  for (int s = 0; s <= N; ++s) {
+    const uint64_t m = __ballot(in && nst == s);
+    mine = (in && nst == s) ? m : mine;
+    if (lane == 0) wc[w][s] = __builtin_popcountll(m);
+  }
+  __syncthreads();
+  if (threadIdx.x <= N) {   // thread s: exclusive scan of bucket s over the waves, one atomic
+    const int s = threadIdx.x;
+    int t = 0;
+    for (int v = 0; v < kClsT / 64; ++v) {
+      const int c = wc[v][s];
+      wc[v][s] = t;
+      t += c;
+    }
+    base[s] = t ? atomicAdd(a.split_count + s, t) : 0;
+  }
+  __syncthreads();
+  if (in) a.split_list[(int64_t)nst * a.B + base[nst] + wc[w][nst] + __builtin_popcountll(mine & ((1ull << lane) - 1))] = (int32_t)i;
+}
 template <int VAR, int N, int NVM>
 __global__ void __launch_bounds__(kClsT) classify_kernel(SolveArgs a) {
   // (one atomic per block and list: per-wave atomics on the two counters
@@ -1963,6 +2011,9 @@ __global__ void __launch_bounds__(kClsT) classify_kernel(SolveArgs a) {
 // ----------------------------------------------------------------------------
 #ifndef HMPC_INST_N
 #error "compile with -DHMPC_INST_N=<horizon>"
+#endif
+#ifndef HMPC_SPLIT_LPT
+#define HMPC_SPLIT_LPT 0
 #endif
 
 #define HMPC_CAT2(a, b) a##b
@@ -2017,8 +2068,22 @@ bool HMPC_CAT(HMPC_CAT(launch_solve_n, HMPC_INST_N), HMPC_LAUNCH_SUFFIX)(int var
     ac.list_count = a.split_count;
     af.list = a.split_list + a.B;
     af.list_count = a.split_count + 1;
+#if HMPC_SPLIT_LPT
+    {   // bucket ranges: the compacted class takes s <= smax, the full class the rest
+      const int smax = (HMPC_CMP_NV - 3 * N) / (variant == 3 ? 3 : 2);
+      ac.list = af.list = a.split_list;
+      ac.list_count = af.list_count = a.split_count;
+      ac.lpt_lo = 0;
+      ac.lpt_hi = smax;
+      af.lpt_lo = smax + 1;
+      af.lpt_hi = N;
+    }
+    if (variant == 3) hipLaunchKernelGGL((classify_buckets_kernel<3, N>), dim3(cb), dim3(kClsT), 0, s, a);
+    else hipLaunchKernelGGL((classify_buckets_kernel<2, N>), dim3(cb), dim3(kClsT), 0, s, a);
+#else
     if (variant == 3) hipLaunchKernelGGL((classify_kernel<3, N, HMPC_CMP_NV>), dim3(cb), dim3(kClsT), 0, s, a);
     else hipLaunchKernelGGL((classify_kernel<2, N, HMPC_CMP_NV>), dim3(cb), dim3(kClsT), 0, s, a);
+#endif
     // the two classes run concurrently: the full kernel on the caller's
     // stream, the compacted one on the split stream, joined back before the
     // overflow pass (one kernel's tail fills with the other's waves)

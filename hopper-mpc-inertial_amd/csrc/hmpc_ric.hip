@@ -1443,8 +1443,7 @@ __global__ void __launch_bounds__(RT) ric_overflow_kernel(SolveArgs a, int N) {
       atomicExch(a.ovf_count, 0);
       atomicExch(a.ovf_count + 1, 0);
       atomicExch(a.ovf_count + 2, 0);
-      atomicExch(a.ovf_count + 3, 0);   // the dense split's class counts
-      atomicExch(a.ovf_count + 4, 0);
+      for (int i = 0; i < a.split_nbkt; ++i) atomicExch(a.ovf_count + 3 + i, 0);   // the dense split's counts
     }
   }
 }
