@@ -122,6 +122,8 @@ def parse():
                          'kernel, f32_refined = fp32 + --refine fp64 corrections (configs[4]); '
                          'others force a kernel for A/B runs')
     ap.add_argument('--refine', type=int, default=5, help='fp64 corrections of f32_refined (5: max|du| <= 1e-6)')
+    ap.add_argument('--order', default='auto', choices=['auto', 'index', 'longest_first'],
+                    help='instance order (hmpc_set_order; auto = longest-first for small batches)')
     ap.add_argument('--cpu-seconds', type=float, default=12.0,
                     help='budget of the bounded CPU-baseline sample, split over its two legs '
                          '(all cores, then one core); 0 disables')
@@ -238,6 +240,7 @@ def main():
                        rh=c['rh'], device=local, precision=args.precision)
     if args.precision == 'f32_refined':
         ctx.set_refinement(args.refine)
+    ctx.set_order(args.order)
     kernel = ctx.kernel_name
     out = dict(u=torch.empty((B, N, 6), dtype=torch.float64, device=dev),
                x=torch.empty((B, N + 1, 12), dtype=torch.float64, device=dev),
@@ -364,7 +367,8 @@ def main():
                        if not args.global_batch else args.global_batch, 'per_gpu_batch': B,
                        'horizon': N, 'variant': args.variant,
                        'plan': 'straight' if args.straight else 'curve', 'mu_sweep': args.mu_sweep,
-                       'precision': args.precision, 'parallelism': f'shard{world}'},
+                       'precision': args.precision, 'order': args.order,
+                       'parallelism': f'shard{world}'},
             'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS,
                          'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic,
                          'bound_effective': f'{prec}_valu_latency',

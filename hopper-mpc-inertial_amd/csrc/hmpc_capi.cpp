@@ -26,6 +26,7 @@ struct hmpc_ctx {
   int uref_mode;
   int precision = HMPC_PREC_F64;
   int refine = 5;   // fp64 corrections of HMPC_PREC_F32_REFINED (hmpc_set_refinement)
+  int order = HMPC_ORDER_AUTO;   // instance order of the dense split / Riccati queue (hmpc_set_order)
   std::string err;
   // staging buffers (host API) and mpcontrol scratch
   void* dbuf = nullptr;
@@ -44,7 +45,9 @@ struct hmpc_ctx {
   // solve whose overflow pass -- which zeroes them at its end -- did not run)
   bool ovf_dirty = true;
   double* rws = nullptr;
-  // dense split launch: the two class lists [2][split_cap]
+  // dense split launch: the two class lists [2][split_cap], or (longest-first
+  // order) up to N + 1 stance-count buckets of split_cap entries; the Riccati
+  // kernel's longest-first queue uses the same buffer for its buckets
   int32_t* split = nullptr;
   int64_t split_cap = 0;
   hipStream_t split_stream = nullptr;   // the compacted class's stream
@@ -98,7 +101,7 @@ hmpc::SolveArgs make_args(hmpc_ctx* c, int64_t B, const double* x_in, const doub
   a.ovf_count = nullptr; a.ovf_list = nullptr; a.rws = nullptr; a.rws_stride = 0;
   a.work = nullptr; a.kws = nullptr; a.kws_stride = 0; a.ric_groups = 0;
   a.split_count = nullptr; a.split_list = nullptr; a.list = nullptr; a.list_count = nullptr;
-  a.lpt_lo = 0; a.lpt_hi = -1; a.split_nbkt = 0;
+  a.lpt = 0; a.lpt_lo = 0; a.lpt_hi = -1; a.split_nbkt = 0;
   a.split_stream = nullptr; a.split_fork = nullptr; a.split_join = nullptr;
   a.precision = c->precision;
   a.refine = c->refine;
@@ -141,6 +144,23 @@ int prepare_ws(hmpc_ctx* c, int64_t B, hmpc::SolveArgs& a) {
 constexpr int kOvfGroups = 128;
 // ints before the overflow list in the counter buffer (see hmpc_ctx::ovf)
 constexpr int kOvfHeader = 16;
+
+// Longest-first order (stance-stage buckets, most stance stages first; the
+// dense split's class lists and the Riccati kernel's work queue) pays where
+// the batch is a few instances per resident wave, so the instances that start
+// last set the step time.  Interleaved A/B (profiles/r04_ab.json): dense
+// configs[1] (B = 4096) 19.9 -> 24.1 M solves/s, B = 16384 -1.7 %, configs[2]
+// (B = 65536) -0.4 %; Riccati N = 60 at 4 instances per workgroup 1.30 ->
+// 1.46 M, configs[3] at 128 per workgroup -6 %.
+constexpr int64_t kDenseLptMaxB = 8192;
+constexpr int64_t kRicLptPerGroup = 8;
+bool longest_first(const hmpc_ctx* c, int64_t B) {
+  if (c->order == HMPC_ORDER_INDEX) return false;
+  if (c->order == HMPC_ORDER_LONGEST_FIRST) return true;
+  if (hmpc::pick_kernel(c->variant, c->N, c->precision) == hmpc::Kernel::Riccati)
+    return B <= kRicLptPerGroup * (int64_t)c->ric_groups;
+  return B <= kDenseLptMaxB;
+}
 
 // Buffers of the dense / Riccati kernels: [overflow count | instance counter |
 // pad | overflow list], the overflow pass's blocks, the Riccati kernel's
@@ -199,7 +219,7 @@ int prepare_ric(hmpc_ctx* c, int64_t B, hmpc::SolveArgs& a) {
       if (c->split) (void)hipFree(c->split);
       c->split = nullptr;
       c->split_cap = 0;
-      // (up to N + 1 stance-count buckets of B entries, HMPC_SPLIT_LPT)
+      // (up to N + 1 stance-count buckets of B entries: longest-first order)
       hipError_t e = hipMalloc(&c->split, sizeof(int32_t) * (size_t)(c->N + 1) * (size_t)B);
       if (e != hipSuccess) { c->err = "split list hipMalloc"; return HMPC_ERR_NOMEM; }
       c->split_cap = B;
@@ -215,6 +235,7 @@ int prepare_ric(hmpc_ctx* c, int64_t B, hmpc::SolveArgs& a) {
     a.split_count = c->ovf + 3;
     a.split_list = c->split;
     a.split_nbkt = c->N + 1;
+    a.lpt = longest_first(c, B) ? 1 : 0;
     a.split_stream = c->split_stream;
     a.split_fork = c->split_fork;
     a.split_join = c->split_join;
@@ -232,6 +253,24 @@ int prepare_ric(hmpc_ctx* c, int64_t B, hmpc::SolveArgs& a) {
     a.kws = c->kws;
     a.kws_stride = hmpc::ric_kws_stride(c->N);
     a.ric_groups = c->ric_groups;
+    // the longest-first work queue: stance-count buckets (<= 13 counters in
+    // the overflow header), lists of B entries each
+    const int nb = hmpc::ric_lpt_buckets(c->N);
+    a.lpt = 0;
+    if (longest_first(c, B) && nb > 0 && nb <= kOvfHeader - 3) {
+      if (B > c->split_cap) {
+        if (c->split) (void)hipFree(c->split);
+        c->split = nullptr;
+        c->split_cap = 0;
+        hipError_t e = hipMalloc(&c->split, sizeof(int32_t) * (size_t)(c->N + 1) * (size_t)B);
+        if (e != hipSuccess) { c->err = "work-queue bucket hipMalloc"; return HMPC_ERR_NOMEM; }
+        c->split_cap = B;
+      }
+      a.split_count = c->ovf + 3;
+      a.split_list = c->split;
+      a.split_nbkt = nb;
+      a.lpt = 1;
+    }
   }
   return HMPC_OK;
 }
@@ -329,7 +368,7 @@ int check_solve_args(hmpc_ctx* c, int64_t B, const void* x_in, const void* x_lin
 
 extern "C" {
 
-int hmpc_version(void) { return 10300; }
+int hmpc_version(void) { return 10400; }
 
 int hmpc_supported_horizons(int variant, int* Ns, int cap) {
   return hmpc::supported_horizons(variant, Ns, cap);
@@ -441,6 +480,16 @@ int hmpc_set_precision(hmpc_ctx* c, int precision) {
     return HMPC_ERR_UNSUPPORTED;
   }
   c->precision = precision;
+  return HMPC_OK;
+}
+
+int hmpc_set_order(hmpc_ctx* c, int order) {
+  if (!c) return HMPC_ERR_ARG;
+  if (order != HMPC_ORDER_AUTO && order != HMPC_ORDER_INDEX && order != HMPC_ORDER_LONGEST_FIRST) {
+    c->err = "order must be HMPC_ORDER_AUTO, _INDEX or _LONGEST_FIRST";
+    return HMPC_ERR_ARG;
+  }
+  c->order = order;
   return HMPC_OK;
 }
 

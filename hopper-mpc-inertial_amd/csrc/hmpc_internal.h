@@ -72,10 +72,13 @@ struct SolveArgs {
   int32_t* split_list;
   const int32_t* list;
   const int32_t* list_count;
-  // HMPC_SPLIT_LPT builds: the class lists are buckets by stance-stage count
-  // (list[s * B ..], count list_count[s]); a launch serves buckets
-  // lpt_lo..lpt_hi, costliest (most stance stages) first.  lpt_hi < 0: one
-  // plain list.  split_nbkt: the bucket counters the overflow pass zeroes.
+  // lpt != 0 (small batches, chosen by the C ABI): longest-first order.  The
+  // dense split's class lists are then buckets by stance-stage count
+  // (list[s * B ..], count list_count[s]) and a launch serves buckets
+  // lpt_lo..lpt_hi, costliest (most stance stages) first (lpt_hi < 0: one
+  // plain list); the Riccati kernel's work queue walks its buckets the same
+  // way.  split_nbkt: the bucket counters the overflow pass zeroes.
+  int lpt;
   int lpt_lo, lpt_hi, split_nbkt;
   // the split's second class runs concurrently on split_stream (forked from
   // and joined back into the caller's stream by the two events); nullptr:
@@ -106,6 +109,9 @@ size_t ric_lds_bytes(int N, int qcap);
 int64_t ric_kws_stride(int N);   // per-workgroup K / Dinv workspace (doubles)
 int64_t ric_rws_stride(int N);   // per-workgroup overflow block: R (6N capacity) + workspace
 int ric_groups(int variant, int N);   // resident workgroups of the main Riccati kernel
+// stance-count buckets of the Riccati kernel's longest-first work queue at
+// horizon N (0: plain index order); their lists take buckets x B ints
+int ric_lpt_buckets(int N);
 bool launch_solve_ric(int variant, int N, const SolveArgs& a, hipStream_t stream);
 // the overflow pass over a.ovf_list (count on the device), <= groups workgroups
 bool launch_solve_ric_overflow(int variant, int N, const SolveArgs& a, int groups, hipStream_t s);

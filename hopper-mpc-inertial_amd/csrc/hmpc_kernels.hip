@@ -614,7 +614,7 @@ solve_kernel(SolveArgs a) {
   // kernel's class list; blocks beyond the list's length have no work
   int64_t b = blockIdx.x;
   if (a.list) {
-    if (a.lpt_hi >= 0) {   // stance-count buckets, costliest first (HMPC_SPLIT_LPT)
+    if (a.lpt_hi >= 0) {   // stance-count buckets, costliest first (a.lpt)
       int i = blockIdx.x, s = a.lpt_hi;
       for (; s >= a.lpt_lo; --s) {
         const int c = a.list_count[s];
@@ -1924,9 +1924,10 @@ solve_kernel(SolveArgs a) {
 // list A at split_list[0..B), list B at split_list[B..2B), lengths in
 // split_count[0..1] (zero at the launch; the overflow pass zeroes them).
 constexpr int kClsT = 1024;   // classify threads per block
-// HMPC_SPLIT_LPT: one list per stance-stage count s = 0..N instead (bucket s
-// at split_list[s B ..), its length in split_count[s]); each class kernel
-// then takes its buckets costliest first (longest-processing-time order).
+// a.lpt (small batches): one list per stance-stage count s = 0..N instead
+// (bucket s at split_list[s B ..), its length in split_count[s]); each class
+// kernel then takes its buckets costliest first (longest-processing-time
+// order: at B = 4096 the slowest instances start first instead of last).
 template <int VAR, int N>
 __global__ void __launch_bounds__(kClsT) classify_buckets_kernel(SolveArgs a) {
   __shared__ int wc[kClsT / 64][N + 1];
@@ -2012,9 +2013,6 @@ __global__ void __launch_bounds__(kClsT) classify_kernel(SolveArgs a) {
 #ifndef HMPC_INST_N
 #error "compile with -DHMPC_INST_N=<horizon>"
 #endif
-#ifndef HMPC_SPLIT_LPT
-#define HMPC_SPLIT_LPT 0
-#endif
 
 #define HMPC_CAT2(a, b) a##b
 #define HMPC_CAT(a, b) HMPC_CAT2(a, b)
@@ -2068,8 +2066,8 @@ bool HMPC_CAT(HMPC_CAT(launch_solve_n, HMPC_INST_N), HMPC_LAUNCH_SUFFIX)(int var
     ac.list_count = a.split_count;
     af.list = a.split_list + a.B;
     af.list_count = a.split_count + 1;
-#if HMPC_SPLIT_LPT
-    {   // bucket ranges: the compacted class takes s <= smax, the full class the rest
+    if (a.lpt && a.split_nbkt >= N + 1) {
+      // bucket ranges: the compacted class takes s <= smax, the full class the rest
       const int smax = (HMPC_CMP_NV - 3 * N) / (variant == 3 ? 3 : 2);
       ac.list = af.list = a.split_list;
       ac.list_count = af.list_count = a.split_count;
@@ -2077,13 +2075,12 @@ bool HMPC_CAT(HMPC_CAT(launch_solve_n, HMPC_INST_N), HMPC_LAUNCH_SUFFIX)(int var
       ac.lpt_hi = smax;
       af.lpt_lo = smax + 1;
       af.lpt_hi = N;
+      if (variant == 3) hipLaunchKernelGGL((classify_buckets_kernel<3, N>), dim3(cb), dim3(kClsT), 0, s, a);
+      else hipLaunchKernelGGL((classify_buckets_kernel<2, N>), dim3(cb), dim3(kClsT), 0, s, a);
+    } else {
+      if (variant == 3) hipLaunchKernelGGL((classify_kernel<3, N, HMPC_CMP_NV>), dim3(cb), dim3(kClsT), 0, s, a);
+      else hipLaunchKernelGGL((classify_kernel<2, N, HMPC_CMP_NV>), dim3(cb), dim3(kClsT), 0, s, a);
     }
-    if (variant == 3) hipLaunchKernelGGL((classify_buckets_kernel<3, N>), dim3(cb), dim3(kClsT), 0, s, a);
-    else hipLaunchKernelGGL((classify_buckets_kernel<2, N>), dim3(cb), dim3(kClsT), 0, s, a);
-#else
-    if (variant == 3) hipLaunchKernelGGL((classify_kernel<3, N, HMPC_CMP_NV>), dim3(cb), dim3(kClsT), 0, s, a);
-    else hipLaunchKernelGGL((classify_kernel<2, N, HMPC_CMP_NV>), dim3(cb), dim3(kClsT), 0, s, a);
-#endif
     // the two classes run concurrently: the full kernel on the caller's
     // stream, the compacted one on the split stream, joined back before the
     // overflow pass (one kernel's tail fills with the other's waves)

@@ -1410,7 +1410,18 @@ __global__ void __launch_bounds__(RT) __attribute__((amdgpu_waves_per_eu(OCC, OC
   double* kw = a.kws + (int64_t)blockIdx.x * a.kws_stride;
   while (true) {
     int b = 0;
-    if (threadIdx.x == 0) b = atomicAdd(a.work, 1);
+    if (threadIdx.x == 0) {
+      b = atomicAdd(a.work, 1);
+      if (a.list && b < a.B) {   // longest-first queue: ticket b in the stance buckets, highest first
+        int s = a.split_nbkt - 1;
+        for (; s > 0; --s) {
+          const int c = a.list_count[s];
+          if (b < c) break;
+          b -= c;
+        }
+        b = a.list[(int64_t)s * a.B + b];
+      }
+    }
     b = __builtin_amdgcn_readfirstlane(b);
     if (b >= a.B) break;
     ric_solve<VAR, 1, OCC == 2 ? kRing2Wave : kRing1Wave, true, NC, CAPC>(a, N, (int64_t)b, ric_sm, ric_sm + L.RM, cap, kw,
@@ -1446,6 +1457,51 @@ __global__ void __launch_bounds__(RT) ric_overflow_kernel(SolveArgs a, int N) {
       for (int i = 0; i < a.split_nbkt; ++i) atomicExch(a.ovf_count + 3 + i, 0);   // the dense split's counts
     }
   }
+}
+
+// The longest-first work queue (a.lpt: a few instances per workgroup, where
+// the queue's last round is the tail): one thread per instance counts
+// its stance stages and appends the instance to bucket nst / W (W stages per
+// bucket, nb <= kLptMax buckets at split_list[bucket * B ..], lengths in
+// split_count[bucket], zero at the launch; the overflow pass zeroes them).
+// The kernel then serves the buckets from the most stance stages down.
+constexpr int kLptT = 1024;
+constexpr int kLptMax = 13;   // bucket counters in the overflow header (hmpc_capi.cpp)
+__global__ void __launch_bounds__(kLptT) ric_buckets_kernel(SolveArgs a, int N, int W) {
+  __shared__ int wc[kLptT / 64][kLptMax];
+  __shared__ int base[kLptMax];
+  const int nb = a.split_nbkt;
+  const int64_t i = (int64_t)blockIdx.x * kLptT + threadIdx.x;
+  const bool in = i < a.B;
+  int k = 0;
+  if (in) {
+    const double* c = a.C + i * a.C_bs;
+    int nst = 0;
+    for (int j = 0; j < N; ++j) nst += c[j] != 0.0 ? 1 : 0;
+    k = min(nst / W, nb - 1);
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint64_t mine = 0;
+  for (int s = 0; s < nb; ++s) {
+    const uint64_t m = __ballot(in && k == s);
+    mine = (in && k == s) ? m : mine;
+    if (lane == 0) wc[w][s] = __builtin_popcountll(m);
+  }
+  __syncthreads();
+  if (threadIdx.x < nb) {   // thread s: exclusive scan of bucket s over the waves, one atomic
+    const int s = threadIdx.x;
+    int t = 0;
+    for (int v = 0; v < kLptT / 64; ++v) {
+      const int c = wc[v][s];
+      wc[v][s] = t;
+      t += c;
+    }
+    base[s] = t ? atomicAdd(a.split_count + s, t) : 0;
+  }
+  __syncthreads();
+  if (in)
+    a.split_list[(int64_t)k * a.B + base[k] + wc[w][k] + __builtin_popcountll(mine & ((1ull << lane) - 1))] =
+        (int32_t)i;
 }
 
 template <typename K>
@@ -1539,11 +1595,27 @@ int ric_groups(int variant, int N) {
   return cus * per;
 }
 
+int ric_lpt_buckets(int N) {
+  if (N < 1) return 0;
+  return N + 1 < kLptMax ? N + 1 : kLptMax;
+}
+
 bool launch_solve_ric(int variant, int N, const SolveArgs& a, hipStream_t s) {
   if (N < 1 || N > kRicNmax || (variant != 2 && variant != 3)) return false;
   if (a.B <= 0) return true;
   if (!a.work || !a.kws || a.ric_groups < 1) return false;
-  return ric_launch_any(variant, N, a, s, nullptr);
+  const int nb = ric_lpt_buckets(N);
+  if (a.lpt && nb > 0 && a.split_list && a.split_count && a.split_nbkt == nb) {
+    const int W = (N + nb) / nb;   // ceil((N + 1) / nb) stance counts per bucket
+    hipLaunchKernelGGL(ric_buckets_kernel, dim3((unsigned)((a.B + kLptT - 1) / kLptT)), dim3(kLptT), 0, s, a, N, W);
+    SolveArgs al = a;
+    al.list = a.split_list;
+    al.list_count = a.split_count;
+    return ric_launch_any(variant, N, al, s, nullptr);
+  }
+  SolveArgs a0 = a;
+  a0.list = nullptr;
+  return ric_launch_any(variant, N, a0, s, nullptr);
 }
 
 bool launch_solve_ric_overflow(int variant, int N, const SolveArgs& a, int groups, hipStream_t s) {

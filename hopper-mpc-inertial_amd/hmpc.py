@@ -23,6 +23,7 @@ VARIANTS = {'3f': 3, '2f': 2, 'cas': 4, 3: 3, 2: 2, 4: 4}
 UREF = {'aliased': 0, 'per_stage': 1}
 PRECISION = {'f64': 0, 'f32': 1, 'f64_generic': 2, 'f64_riccati': 3, 'f64_dense': 4, 'f32_generic': 5,
              'f32_refined': 6}
+ORDER = {'auto': 0, 'index': 1, 'longest_first': 2}
 
 # symbol -> (restype, argtypes); every symbol declared in include/hmpc.h
 _D = ctypes.POINTER(ctypes.c_double)
@@ -38,6 +39,7 @@ SIGNATURES = {
     'hmpc_solve_batch': (ctypes.c_int, [_VP, ctypes.c_int64] + [_VP] * 11 + [_VP]),
     'hmpc_solve_batch_stats': (ctypes.c_int, [_VP, ctypes.c_int64] + [_VP] * 12 + [_VP]),
     'hmpc_set_refinement': (ctypes.c_int, [_VP, ctypes.c_int]),
+    'hmpc_set_order': (ctypes.c_int, [_VP, ctypes.c_int]),
     'hmpc_solve_batch_host': (ctypes.c_int, [_VP, ctypes.c_int64] + [_VP] * 11),
     'hmpc_mpcontrol_batch': (ctypes.c_int, [_VP, ctypes.c_int64, ctypes.c_int] + [_VP] * 10 + [_VP]),
     'hmpc_mpcontrol_plan_batch': (ctypes.c_int, [_VP, ctypes.c_int64, ctypes.c_int, _VP, _VP, _VP,
@@ -162,6 +164,11 @@ class Context:
     def set_refinement(self, corrections):
         """fp64 corrections of precision 'f32_refined' (hmpc_set_refinement)."""
         self._check(self._lib.hmpc_set_refinement(self._h, int(corrections)), 'hmpc_set_refinement')
+
+    def set_order(self, order):
+        """Instance order of later solves (hmpc_set_order): 'auto' (longest-first
+        for small batches), 'index' or 'longest_first'.  Results do not depend on it."""
+        self._check(self._lib.hmpc_set_order(self._h, ORDER[order]), 'hmpc_set_order')
 
     @property
     def kernel_name(self):

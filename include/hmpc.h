@@ -97,7 +97,8 @@ typedef struct hmpc_ctx hmpc_ctx;
 /* ABI version (major*10000 + minor*100 + patch): 1.2.0 = 1.0 + the fp32 dense
    build, HMPC_PREC_F64_RICCATI / _F64_DENSE / _F32_GENERIC, hmpc_kernel_name,
    hmpc_active_capacity, hmpc_plan_batch, hmpc_gait_batch, HMPC_VARIANT_CAS;
-   1.3.0 = + hmpc_solve_batch_stats, HMPC_PREC_F32_REFINED, hmpc_set_refinement */
+   1.3.0 = + hmpc_solve_batch_stats, HMPC_PREC_F32_REFINED, hmpc_set_refinement;
+   1.4.0 = + hmpc_set_order */
 int hmpc_version(void);
 
 /* Which horizons have a dedicated (one- or two-wavefront) kernel for
@@ -244,11 +245,25 @@ int hmpc_set_precision(hmpc_ctx* ctx, int precision);
    fp64 rollout + adjoint and two fp32 sweeps per instance). */
 int hmpc_set_refinement(hmpc_ctx* ctx, int corrections);
 
+/* Instance order of later solves (results do not depend on it):
+     HMPC_ORDER_AUTO            longest-first for small batches, where the
+                                instances that start last set the step time
+                                (dense split B <= 8192; Riccati kernel up to 8
+                                instances per resident workgroup), else index
+     HMPC_ORDER_INDEX           batch index order
+     HMPC_ORDER_LONGEST_FIRST   stance-stage buckets, most stance stages first
+   Longest-first measured +21 % at configs[1] (B = 4096) and +12 % at the
+   Runner's N = 60 (B = 4096); -0.4 % at configs[2], -6 % at configs[3]. */
+#define HMPC_ORDER_AUTO 0
+#define HMPC_ORDER_INDEX 1
+#define HMPC_ORDER_LONGEST_FIRST 2
+int hmpc_set_order(hmpc_ctx* ctx, int order);
+
 /* Name of the solve kernel this context's (variant, N, precision) runs on,
    as rocprofv3 demangles it, e.g. "hmpc::ric_kernel<3, 2, 0, 0>"; a split launch names
-   every class kernel, "hmpc::solve_kernel_p<3, 10, double, 48, 13> + hmpc::solve_kernel_p<3, 10,
+   every class kernel, "hmpc::solve_kernel<3, 10, double, 48, 13> + hmpc::solve_kernel<3, 10,
    double, 0, 0>" (the narrowest first; 2f's full class is the 5N-wide
-   "hmpc::solve_kernel_p<2, 10, double, 50, 20>").  Static string, "" when none.  For
+   "hmpc::solve_kernel<2, 10, double, 50, 20>").  Static string, "" when none.  For
    benchmark records and profiles. */
 const char* hmpc_kernel_name(hmpc_ctx* ctx);
 

@@ -34,7 +34,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_version_and_horizons():
     lib = hmpc.load()
-    assert lib.hmpc_version() == 10300   # 1.3: + hmpc_solve_batch_stats (1.2: planner, CasADi, precisions 4-5, capacity)
+    assert lib.hmpc_version() == 10400   # 1.4: + hmpc_set_order (1.3: stats, refinement; 1.2: planner, CasADi, precisions 4-5, capacity)
     hs = hmpc.supported_horizons('3f')
     assert 10 in hs and 20 in hs
     assert hmpc.supported_horizons('2f') == hs
@@ -51,6 +51,8 @@ def test_argument_errors_do_not_need_a_gpu():
     assert lib.hmpc_create(ctypes.byref(h), 3, 129, 0.02, 7.5, 9.807, 1.0, J, r, 0, 0) == -2
     assert lib.hmpc_destroy(None) == -1
     assert lib.hmpc_set_precision(None, 1) == -1
+    assert lib.hmpc_set_order(None, 0) == -1
+    assert lib.hmpc_set_refinement(None, 2) == -1
 
 
 def test_missing_library_fails_loudly(tmp_path):

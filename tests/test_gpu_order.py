@@ -1,0 +1,92 @@
+"""Instance order (hmpc_set_order): the dense split's class lists and the
+Riccati kernel's work queue served longest-first (stance-stage buckets, most
+stance stages first) or in batch index order.  Each instance is solved by the
+same kernel either way, so the results must be bit-identical between the
+orders, and equal to the C port's; the overflow pass and the self-resetting
+bucket counters must survive alternating orders on one context."""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip('torch')
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope='module')
+def hm():
+    if not torch.cuda.is_available():
+        pytest.fail('GPU tests need an MI355X (torch.cuda.is_available() is False)')
+    import hmpc
+    return hmpc
+
+
+def context(hm, variant, N):
+    import hmpc_plan
+    c = hmpc_plan.runner_constants()
+    return hm.Context(variant, N, t=c['t'], m=c['m'], g=c['g'], mu=1.0, Jinv=c['Jinv'], rh=c['rh'])
+
+
+@pytest.mark.parametrize('variant,N,B,curve,musweep', [
+    ('3f', 10, 3000, True, False),     # dense split, 3f
+    ('2f', 10, 2048, False, False),    # dense split, 2f (5N-wide full class)
+    ('3f', 20, 1500, False, True),     # Riccati, 2 waves / SIMD
+    ('3f', 60, 300, False, False),     # Riccati, the Runner's horizon
+])
+def test_orders_agree_bit_for_bit(hm, variant, N, B, curve, musweep):
+    import hmpc_plan
+    from oracle import port
+    inst = hmpc_plan.sample_instances(B, N, curve=curve, seed=77 + N,
+                                      mu_sweep=(0.3, 1.2) if musweep else None)
+    cx = context(hm, variant, N)
+    args = (inst['x_in'], inst['x_lin'], inst['x_ref'], inst['pf'], inst['C'])
+    res = {}
+    # alternate on one context: the bucket / class counters reset themselves
+    for order in ('longest_first', 'index', 'longest_first', 'auto'):
+        cx.set_order(order)
+        r = cx.solve_host(*args, mu=inst['mu'])
+        if order in res:
+            for k in r:
+                assert np.array_equal(r[k], res[order][k]), (order, k)
+        res.setdefault(order, r)
+    cx.close()
+    a, b = res['longest_first'], res['index']
+    for k in a:
+        assert np.array_equal(a[k], b[k]), k
+    n = min(B, 256)
+    ref = port.solve_batch(variant, N, *(v[:n] for v in args), mu=inst['mu'][:n], nthreads=16)
+    assert np.array_equal(a['status'][:n], ref['status'])
+    ok = ref['status'] == 0
+    assert np.abs(a['u'][:n][ok] - ref['u'][ok]).max() <= 1e-6
+
+
+def test_longest_first_with_overflow(hm):
+    """Instances whose active set outgrows the kernel (forced by large initial
+    velocities) go to the overflow pass under either order."""
+    import hmpc_plan
+    from oracle import port
+    N, B = 10, 512
+    inst = hmpc_plan.sample_instances(B, N, curve=True, seed=5, mu_sweep=(0.2, 0.2))
+    rng = np.random.default_rng(5)
+    inst['x_in'][:, 9:12] += rng.choice([-1, 1], (B, 3)) * rng.uniform(0.7, 1.0, (B, 3)) * 50.0
+    inst['x_in'][:, 6:8] += rng.choice([-1, 1], (B, 2)) * rng.uniform(0.7, 1.0, (B, 2)) * 8.0
+    inst['x_lin'][:, 0] = inst['x_in']
+    args = (inst['x_in'], inst['x_lin'], inst['x_ref'], inst['pf'], inst['C'])
+    cx = context(hm, '3f', N)
+    cx.set_order('longest_first')
+    a = cx.solve_host(*args, mu=inst['mu'])
+    cx.set_order('index')
+    b = cx.solve_host(*args, mu=inst['mu'])
+    cx.close()
+    for k in a:
+        assert np.array_equal(a[k], b[k]), k
+    ref = port.solve_batch('3f', N, *args, mu=inst['mu'], nthreads=16)
+    assert np.array_equal(a['status'], ref['status'])
+    ok = ref['status'] == 0
+    assert np.abs(a['u'][ok] - ref['u'][ok]).max() <= 1e-6
+
+
+def test_set_order_rejects_unknown(hm):
+    cx = context(hm, '3f', 10)
+    with pytest.raises(hm.HmpcError):
+        cx._check(cx._lib.hmpc_set_order(cx._h, 7), 'hmpc_set_order')
+    cx.close()
