@@ -332,17 +332,9 @@ __device__ __forceinline__ int loff(int r) { return (r * (r + 1)) >> 1; }
 
 // prefetch depth (steps) of the two-wave sweeps' LDS ring (two loads a step:
 // lgkmcnt waits of 2 kRing2 - 2 <= 15)
-#ifndef HMPC_RING2
-#define HMPC_RING2 8
-#endif
-constexpr int kRing2 = HMPC_RING2;
-static_assert(kRing2 == 4 || kRing2 == 8, "ring depth");
-// and of the one-wave sweeps (one load a step)
-#ifndef HMPC_RING1
-#define HMPC_RING1 4
-#endif
-constexpr int kRing1 = HMPC_RING1;
-static_assert(kRing1 == 4 || kRing1 == 8, "ring depth");
+constexpr int kRing2 = 8;
+// and of the one-wave sweeps (one load a step; 8 measured -1.4 %)
+constexpr int kRing1 = 4;
 
 // ----------------------------------------------------------------------------
 // triangular sweeps.  The factor is kept as the unit lower M = L diag(L)^-1,
@@ -543,30 +535,21 @@ __device__ __forceinline__ real tri_bwd(real acc, const real* Mc, const real* ze
 #define HMPC_TOC(slot, v) ((void)0)
 #endif
 
-// issue priority of the chain-bound phases: 0 off, 1 (default) the Cholesky
-// through the active set, 2 the Cholesky only.  A wave in its dependent
-// pivot/sweep chains issues first; the co-resident wave's throughput phases
-// (sweeps of phase 2, Hessian rows, outputs) fill the gaps: +0.4-0.9 %.
-#ifndef HMPC_PRIO
-#define HMPC_PRIO 1
-#endif
-// Between the split's classes: the full kernel's waves hold the small-batch
-// critical path (its instances are the longest), so they run at priority 2
-// outside the chain phases (3 inside), the compacted kernel's at 0 / 1.
-// configs[1] +1.6 %, configs[2] and B = 16384 unchanged (profiles/r03_ab.json).
-#ifndef HMPC_PRIO_CMP
-#define HMPC_PRIO_CMP 1
-#endif
-#ifndef HMPC_PRIO_FULL_BASE
-#define HMPC_PRIO_FULL_BASE 2
-#endif
+// issue priority of the chain-bound phases (the Cholesky through the active
+// set): a wave in its dependent pivot/sweep chains issues first; the
+// co-resident wave's throughput phases (sweeps of phase 2, Hessian rows,
+// outputs) fill the gaps: +0.4-0.9 %.  Between the split's classes: the full
+// kernel's waves hold the small-batch critical path (its instances are the
+// longest), so they run at priority 2 outside the chain phases (3 inside),
+// the compacted kernel's at 0 / 1: configs[1] +1.6 %, configs[2] and
+// B = 16384 unchanged (profiles/r03_ab.json).
+constexpr int kPrioCmp = 1;
+constexpr int kPrioFullBase = 2;
 #ifndef HMPC_WAVES_PER_EU
 #define HMPC_WAVES_PER_EU(W) ((W) == 1 ? 2 : 1)
 #endif
 // waves / SIMD of the compacted kernel (NVM > 0)
-#ifndef HMPC_CMP_WAVES
-#define HMPC_CMP_WAVES 3
-#endif
+constexpr int kCmpWaves = 3;
 // the widest compacted rows that fit 3 waves / SIMD (<= 168 VGPRs); a wider
 // compacted kernel (2f's 5N-wide full class) runs 2 waves like the full one
 constexpr int kCmp3W = 48;
@@ -588,7 +571,7 @@ __device__ __forceinline__ const SolveArgs& opaque_args(const SolveArgs& a) {
 
 template <int VAR, int N, typename R, int NVM = 0, int QM = 0>
 __global__ void __launch_bounds__((Lay<N, NVM, QM>::NT),
-                                  (NVM > 0 && NVM <= kCmp3W ? HMPC_CMP_WAVES
+                                  (NVM > 0 && NVM <= kCmp3W ? kCmpWaves
                                    : (NVM > 0 ? 2 : HMPC_WAVES_PER_EU((Lay<N, NVM, QM>::W)))))
 solve_kernel(SolveArgs a) {
   static_assert(sizeof(R) == sizeof(real), "one arithmetic type per build");
@@ -607,7 +590,7 @@ solve_kernel(SolveArgs a) {
 #endif
   HMPC_STAMP(0);
   constexpr bool kCmpCls = NVM > 0 && NVM <= kCmp3W;   // the split's compacted class
-  if constexpr (HMPC_PRIO_FULL_BASE != 0 && !kCmpCls) __builtin_amdgcn_s_setprio(HMPC_PRIO_FULL_BASE);
+  if constexpr (!kCmpCls) __builtin_amdgcn_s_setprio(kPrioFullBase);
 
   const int tid = threadIdx.x;
   // split launch (launch_solve_n<N>): block i solves the i-th instance of this
@@ -1034,7 +1017,7 @@ solve_kernel(SolveArgs a) {
   real wv = -hv;   // the forward sweep's accumulator (phase 4)
   __syncthreads();   // union A (XLIN/XREF/PF/S/DG) is dead from here on
   HMPC_STAMP(4);
-  if constexpr (HMPC_PRIO != 0) __builtin_amdgcn_s_setprio(kCmpCls ? HMPC_PRIO_CMP : 3);
+  __builtin_amdgcn_s_setprio(kCmpCls ? kPrioCmp : 3);
 
   int status = ST_SOLVED;
   real dinv = 0.0;
@@ -1269,7 +1252,6 @@ solve_kernel(SolveArgs a) {
     if constexpr (W == 1) dinv = active_lane ? dinv : real(1);   // padding: never stepped
   }
   HMPC_STAMP(5);
-  if constexpr (HMPC_PRIO == 2) __builtin_amdgcn_s_setprio(kCmpCls ? 0 : HMPC_PRIO_FULL_BASE);
 
   const real* Lc = sm + L::LC;
   const real* zero = sm + L::ZR;
@@ -1595,9 +1577,6 @@ solve_kernel(SolveArgs a) {
   // it (or any non-solved fp32 instance) goes to the fp64 overflow pass.
   if constexpr (kRefine) {
     static_assert(W == 1, "the refinement runs in one-wave kernels");
-#ifdef HMPC_MARKS
-    asm volatile(";@@PHASE 61");
-#endif
     if (uni(status) != ST_SOLVED && a.ovf_count) status = ST_OVERFLOW;
     if (uni(status) == ST_SOLVED) {
       const SolveArgs& ka = opaque_args(a);   // (fresh loads of the arguments)
@@ -1820,7 +1799,7 @@ solve_kernel(SolveArgs a) {
     }
   }
   HMPC_STAMP(7);
-  if constexpr (HMPC_PRIO != 0) __builtin_amdgcn_s_setprio(kCmpCls ? 0 : HMPC_PRIO_FULL_BASE);
+  __builtin_amdgcn_s_setprio(kCmpCls ? 0 : kPrioFullBase);
 
   // an overflowed instance writes nothing but its status and its place in
   // the overflow list (x_lin may be this solve's input, mpcontrol shift)
