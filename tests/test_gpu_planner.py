@@ -135,7 +135,11 @@ def test_gait_schedule_before_t0(cx):
 def test_plan_index_errors_are_reported(cx):
     """Where the reference raises IndexError (a footstep peak pushed outside
     the plan by step_adjustment, src/robotrunner.py:211-216) hmpc_plan_batch
-    returns HMPC_ERR_ARG instead of a silently clamped plan."""
+    returns HMPC_ERR_ARG instead of a silently clamped plan.  The error is
+    raised only for a peak the footstep counter reads, as in the reference;
+    no Runner configuration reaches an out-of-range peak that is never read
+    (t_p 0.3-1.6, phi_switch 0.2-0.8 and step_adjustment 0-2000 searched with
+    the host planner), so only the read case has a test."""
     import hmpc
     import hmpc_plan as hp
     cfg = hp.RunnerConfig(N_run=2000, N=10)
