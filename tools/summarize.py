@@ -127,4 +127,4 @@ def main(tag, cfgs):
 
 
 if __name__ == '__main__':
-    main(sys.argv[1], sys.argv[2:] or ['n10', 'n20', 'n60', 'n10_2f', 'n10_f32'])
+    main(sys.argv[1], sys.argv[2:] or ['n10', 'n20', 'n60', 'n10_2f', 'n10_f32', 'n10_f32r'])
