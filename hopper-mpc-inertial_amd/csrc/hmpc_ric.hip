@@ -1436,6 +1436,13 @@ template <int VAR>
 __global__ void __launch_bounds__(RT) ric_overflow_kernel(SolveArgs a, int N) {
   extern __shared__ __attribute__((aligned(16))) double ric_sm[];
   const int n = *a.ovf_count;
+  if (n == 0) {
+    // nothing to re-solve (the usual case): no block depends on the counters
+    // any more, so block 0 zeroes them at once, without the done counter's
+    // one serialised atomic per workgroup
+    if (blockIdx.x == 0 && (int)threadIdx.x < 3 + a.split_nbkt) a.ovf_count[threadIdx.x] = 0;
+    return;
+  }
   double* Rm = a.rws + (int64_t)blockIdx.x * a.rws_stride;
   double* kw = Rm + (a.rws_stride - ric_kws_doubles(N));
   SolveArgs a2 = a;
