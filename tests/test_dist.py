@@ -1,4 +1,4 @@
-"""Multi-process path on CPU with gloo, world_size 2: each rank
+"""Multi-process path on CPU with gloo, world_size 2 and 4: each rank
 draws its contiguous shard from (seed, global index), solves it (here with the
 oracle's C port standing in for the GPU kernel) and all-gathers objective +
 status; every rank must end with exactly the single-process result."""
@@ -74,7 +74,7 @@ def _worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize('world', [2])
+@pytest.mark.parametrize('world', [2, 4])
 def test_sharded_allgather_equals_single_process(world):
     import subprocess
     subprocess.check_call(['make', '-s', '-C', os.path.join(ROOT, 'oracle')])
@@ -98,8 +98,10 @@ def test_sharded_allgather_equals_single_process(world):
     # single-process solve bit for bit
     gobj, gst = _solve(0, 2 * PER_RANK + 1)
     shards = sorted((r[5], r[6], r[7], r[8]) for r in res)
-    assert shards[0][0] == 0 and shards[0][0] + shards[0][1] == shards[1][0]
-    assert shards[1][0] + shards[1][1] == 2 * PER_RANK + 1
+    assert shards[0][0] == 0
+    for lo, hi in zip(shards, shards[1:]):
+        assert lo[0] + lo[1] == hi[0]
+    assert shards[-1][0] + shards[-1][1] == 2 * PER_RANK + 1
     assert np.array_equal(np.concatenate([sh[2] for sh in shards]), gobj)
     assert np.array_equal(np.concatenate([sh[3] for sh in shards]), gst)
     for r in res:   # the uneven exchange: every rank holds the whole global batch
