@@ -22,8 +22,10 @@ pids=()
 # the split launch's compacted kernel (at most NV free variables, active-set
 # capacity Q, 3 waves / SIMD) per horizon: "N:NV:Q" (CMP="" disables)
 CMP=${CMP-"10:48:13"}
-cmp_flags() {
-  for e in $CMP; do
+# the same for the fp32 builds (4 waves / SIMD; F32_CMP="" disables)
+F32_CMP=${F32_CMP-"10:48:13"}
+cmp_flags() {   # horizon [list]
+  for e in ${2-$CMP}; do
     IFS=: read -r cn cv cq <<< "$e"
     if [ "$cn" = "$1" ]; then echo "-DHMPC_CMP_NV=$cv -DHMPC_CMP_Q=$cq"; fi
   done
@@ -40,10 +42,18 @@ for n in $HORIZONS; do
   while [ "$(jobs -rp | wc -l)" -ge "$JOBS" ]; do sleep 1; done
 done
 for n in $F32_HORIZONS; do
-  # fp32: 3 waves / SIMD fit (<= 168 VGPRs, 9.9 KB LDS) without spilling
+  # fp32: 3 waves / SIMD fit (<= 168 VGPRs, 9.9 KB LDS) without spilling;
+  # split like fp64, the compacted class at 4 waves / SIMD
+  F32C=$(cmp_flags $n "$F32_CMP")
   $HIPCC $FLAGS -DHMPC_INST_N=$n -DHMPC_REAL=float -DHMPC_LAUNCH_SUFFIX=_f32 "-DHMPC_WAVES_PER_EU(W)=$F32_WAVES" \
-    -c csrc/hmpc_kernels.hip -o $BDIR/hmpc_kernels_n${n}_f32.o "$@" &
+    $F32C -c ${KSRC:-csrc/hmpc_kernels.hip} -o $BDIR/hmpc_kernels_n${n}_f32.o "$@" &
   pids+=($!)
+  if [ -n "$F32C" ]; then
+    $HIPCC $FLAGS -DHMPC_INST_N=$n -DHMPC_REAL=float -DHMPC_LAUNCH_SUFFIX=_f32 "-DHMPC_WAVES_PER_EU(W)=$F32_WAVES" \
+      $F32C -DHMPC_CMP_ONLY -c ${KSRC:-csrc/hmpc_kernels.hip} -o $BDIR/hmpc_kernels_n${n}_f32_cmp.o "$@" &
+    pids+=($!)
+    CMPOBJS="$CMPOBJS $BDIR/hmpc_kernels_n${n}_f32_cmp.o"
+  fi
   # fp32 + fp64 refinement (HMPC_PREC_F32_REFINED)
   $HIPCC $FLAGS -DHMPC_INST_N=$n -DHMPC_REAL=float -DHMPC_F32_REFINE=1 -DHMPC_LAUNCH_SUFFIX=_f32r \
     "-DHMPC_WAVES_PER_EU(W)=$F32_WAVES" -c csrc/hmpc_kernels.hip -o $BDIR/hmpc_kernels_n${n}_f32r.o "$@" &

@@ -214,7 +214,9 @@ int prepare_ric(hmpc_ctx* c, int64_t B, hmpc::SolveArgs& a) {
   // the dense kernel's split launch (compacted kernel for the instances with
   // few free variables): class counts next to the overflow counters, which
   // the overflow pass zeroes together at its end
-  if (k == hmpc::Kernel::Dense && hmpc::dense_split_nv(c->N, 0) > 0 && c->N + 1 <= kOvfHeader - 3) {
+  const bool split = (k == hmpc::Kernel::Dense && hmpc::dense_split_nv(c->N, 0) > 0) ||
+                     (k == hmpc::Kernel::DenseF32 && hmpc::dense_split_nv(c->N, 1) > 0);
+  if (split && c->N + 1 <= kOvfHeader - 3) {
     if (B > c->split_cap) {
       if (c->split) (void)hipFree(c->split);
       c->split = nullptr;

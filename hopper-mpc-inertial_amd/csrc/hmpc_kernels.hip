@@ -548,10 +548,11 @@ constexpr int kPrioFullBase = 2;
 #ifndef HMPC_WAVES_PER_EU
 #define HMPC_WAVES_PER_EU(W) ((W) == 1 ? 2 : 1)
 #endif
-// waves / SIMD of the compacted kernel (NVM > 0)
-constexpr int kCmpWaves = 3;
-// the widest compacted rows that fit 3 waves / SIMD (<= 168 VGPRs); a wider
-// compacted kernel (2f's 5N-wide full class) runs 2 waves like the full one
+// waves / SIMD of the split's compacted class (NVM <= kCmp3W): fp64 3
+// (<= 168 VGPRs), fp32 4 (<= 128, 12 B/lane of spill); a wider compacted
+// kernel (2f's 5N-wide full class) runs like the full one, fp64 2, fp32 3
+constexpr int kCmpWaves = sizeof(real) == 4 ? 4 : 3;
+constexpr int kWideCmpWaves = sizeof(real) == 4 ? 3 : 2;
 constexpr int kCmp3W = 48;
 // The kernel's argument block through an opaque kernarg-segment pointer:
 // reads through it are fresh scalar loads where they stand, so the compiler
@@ -572,7 +573,7 @@ __device__ __forceinline__ const SolveArgs& opaque_args(const SolveArgs& a) {
 template <int VAR, int N, typename R, int NVM = 0, int QM = 0>
 __global__ void __launch_bounds__((Lay<N, NVM, QM>::NT),
                                   (NVM > 0 && NVM <= kCmp3W ? kCmpWaves
-                                   : (NVM > 0 ? 2 : HMPC_WAVES_PER_EU((Lay<N, NVM, QM>::W)))))
+                                   : (NVM > 0 ? kWideCmpWaves : HMPC_WAVES_PER_EU((Lay<N, NVM, QM>::W)))))
 solve_kernel(SolveArgs a) {
   static_assert(sizeof(R) == sizeof(real), "one arithmetic type per build");
   using L = Lay<N, NVM, QM>;
@@ -2002,18 +2003,21 @@ __global__ void __launch_bounds__(kClsT) classify_kernel(SolveArgs a) {
 #if defined(HMPC_CMP_NV) && HMPC_CMP_NV > 0
 // the split's compacted kernel launches from a translation unit of its own
 // (-DHMPC_CMP_ONLY): the objects build in parallel
-bool HMPC_CAT(launch_cmp_n, HMPC_INST_N)(int variant, const SolveArgs& a, hipStream_t s);
+// (one launcher per build flavour: HMPC_LAUNCH_SUFFIX, e.g. _f32)
+#define HMPC_CMP_LAUNCH HMPC_CAT(HMPC_CAT(launch_cmp_n, HMPC_INST_N), HMPC_LAUNCH_SUFFIX)
+#define HMPC_FULL2F_LAUNCH HMPC_CAT(HMPC_CAT(launch_full2f_n, HMPC_INST_N), HMPC_LAUNCH_SUFFIX)
+bool HMPC_CMP_LAUNCH(int variant, const SolveArgs& a, hipStream_t s);
 // 2f's full class: at most 5N free variables (3N torques + 2N stance forces;
 // f_y is fixed), so a 5N-wide compacted kernel replaces the 6N-wide full one
 // when 5N rows fit one wave (same capacity as the full kernel)
 #if 5 * HMPC_INST_N > HMPC_CMP_NV && 5 * HMPC_INST_N <= 64
 #define HMPC_FULL2F_NV (5 * HMPC_INST_N)
 #define HMPC_FULL2F_Q (Lay<HMPC_INST_N>::QMAX)
-bool HMPC_CAT(launch_full2f_n, HMPC_INST_N)(const SolveArgs& a, hipStream_t s);
+bool HMPC_FULL2F_LAUNCH(const SolveArgs& a, hipStream_t s);
 #endif
 #endif
 #ifdef HMPC_CMP_ONLY
-bool HMPC_CAT(launch_cmp_n, HMPC_INST_N)(int variant, const SolveArgs& a, hipStream_t s) {
+bool HMPC_CMP_LAUNCH(int variant, const SolveArgs& a, hipStream_t s) {
   if (variant == 3)
     hipLaunchKernelGGL((solve_kernel<3, HMPC_INST_N, real, HMPC_CMP_NV, HMPC_CMP_Q>), dim3((unsigned)a.B), dim3(64), 0, s, a);
   else
@@ -2021,7 +2025,7 @@ bool HMPC_CAT(launch_cmp_n, HMPC_INST_N)(int variant, const SolveArgs& a, hipStr
   return true;
 }
 #ifdef HMPC_FULL2F_NV
-bool HMPC_CAT(launch_full2f_n, HMPC_INST_N)(const SolveArgs& a, hipStream_t s) {
+bool HMPC_FULL2F_LAUNCH(const SolveArgs& a, hipStream_t s) {
   hipLaunchKernelGGL((solve_kernel<2, HMPC_INST_N, real, HMPC_FULL2F_NV, HMPC_FULL2F_Q>), dim3((unsigned)a.B), dim3(64), 0,
                      s, a);
   return true;
@@ -2071,11 +2075,11 @@ bool HMPC_CAT(HMPC_CAT(launch_solve_n, HMPC_INST_N), HMPC_LAUNCH_SUFFIX)(int var
     }
     if (variant == 3) hipLaunchKernelGGL((solve_kernel<3, N, real>), dim3((unsigned)a.B), dim3(NT), 0, s, af);
 #ifdef HMPC_FULL2F_NV
-    else HMPC_CAT(launch_full2f_n, HMPC_INST_N)(af, s);
+    else HMPC_FULL2F_LAUNCH(af, s);
 #else
     else hipLaunchKernelGGL((solve_kernel<2, N, real>), dim3((unsigned)a.B), dim3(NT), 0, s, af);
 #endif
-    HMPC_CAT(launch_cmp_n, HMPC_INST_N)(variant, ac, s2);
+    HMPC_CMP_LAUNCH(variant, ac, s2);
     if (s2 != s) {
       if (hipEventRecord(a.split_join, s2) != hipSuccess) return false;
       if (hipStreamWaitEvent(s, a.split_join, 0) != hipSuccess) return false;

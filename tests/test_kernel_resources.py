@@ -92,6 +92,16 @@ def test_dense_split_budgets(kernels, v):
     assert full['.private_segment_fixed_size'] == 0 and full['.vgpr_spill_count'] == 0
 
 
+@pytest.mark.parametrize('v', [3, 2])
+def test_dense_fp32_split_budgets(kernels, v):
+    (cmp,) = kernels[solve(v, 10, 'f', 48, 13)]
+    assert cmp['.vgpr_count'] <= 128 and cmp['.agpr_count'] == 0   # 4 waves / SIMD
+    assert cmp['.private_segment_fixed_size'] <= 16                # 12 / 8 B/lane measured
+    if v == 2:
+        (full,) = kernels[solve(2, 10, 'f', 50, 20)]
+        assert full['.vgpr_count'] <= 168 and full['.private_segment_fixed_size'] == 0   # 3 waves
+
+
 def test_dense_fp32_builds(kernels):
     # the fp32 kernel and its fp64-refinement build share a name: the plain
     # one has the smaller LDS block
