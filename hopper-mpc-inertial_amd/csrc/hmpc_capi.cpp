@@ -55,6 +55,9 @@ struct hmpc_ctx {
   // Riccati kernel: per-workgroup K / Dinv workspace of its resident grid
   double* kws = nullptr;
   int ric_groups = 0;
+  // Riccati factorisation kernel: K / Dinv per instance (kinst_cap instances)
+  double* kinst = nullptr;
+  int64_t kinst_cap = 0;
   // planner scratch (footstep counter, peak lists)
   void* plan_scratch = nullptr;
   int64_t plan_scratch_bytes = 0;
@@ -100,6 +103,7 @@ hmpc::SolveArgs make_args(hmpc_ctx* c, int64_t B, const double* x_in, const doub
   a.ws = nullptr; a.ws_stride = 0; a.ws_groups = 0;
   a.ovf_count = nullptr; a.ovf_list = nullptr; a.rws = nullptr; a.rws_stride = 0;
   a.work = nullptr; a.kws = nullptr; a.kws_stride = 0; a.ric_groups = 0;
+  a.kinst = nullptr; a.kinst_stride = 0;
   a.split_count = nullptr; a.split_list = nullptr; a.list = nullptr; a.list_count = nullptr;
   a.lpt = 0; a.lpt_lo = 0; a.lpt_hi = -1; a.split_nbkt = 0;
   a.split_stream = nullptr; a.split_fork = nullptr; a.split_join = nullptr;
@@ -169,6 +173,7 @@ int prepare_ric(hmpc_ctx* c, int64_t B, hmpc::SolveArgs& a) {
   const hmpc::Kernel k = hmpc::pick_kernel(c->variant, c->N, c->precision);
   a.ovf_count = nullptr; a.ovf_list = nullptr; a.rws = nullptr; a.rws_stride = 0;
   a.work = nullptr; a.kws = nullptr; a.kws_stride = 0; a.ric_groups = 0;
+  a.kinst = nullptr; a.kinst_stride = 0;
   a.split_count = nullptr; a.split_list = nullptr;
   if (k == hmpc::Kernel::Cas) {   // instance counter + R slots, no overflow pass
     if (!c->ovf) {
@@ -255,6 +260,20 @@ int prepare_ric(hmpc_ctx* c, int64_t B, hmpc::SolveArgs& a) {
     a.kws = c->kws;
     a.kws_stride = hmpc::ric_kws_stride(c->N);
     a.ric_groups = c->ric_groups;
+    // the factorisation kernel's per-instance K / Dinv blocks
+    const int64_t ks = hmpc::ric_kinst_stride(c->N, B);
+    if (ks > 0) {
+      if (B > c->kinst_cap) {
+        if (c->kinst) (void)hipFree(c->kinst);
+        c->kinst = nullptr;
+        c->kinst_cap = 0;
+        hipError_t e = hipMalloc(&c->kinst, sizeof(double) * (size_t)ks * (size_t)B);
+        if (e != hipSuccess) { c->err = "Riccati factorisation hipMalloc"; return HMPC_ERR_NOMEM; }
+        c->kinst_cap = B;
+      }
+      a.kinst = c->kinst;
+      a.kinst_stride = ks;
+    }
     // the longest-first work queue: stance-count buckets (<= 13 counters in
     // the overflow header), lists of B entries each
     const int nb = hmpc::ric_lpt_buckets(c->N);
@@ -410,6 +429,7 @@ int hmpc_destroy(hmpc_ctx* c) {
   if (c->split_fork) (void)hipEventDestroy(c->split_fork);
   if (c->split_join) (void)hipEventDestroy(c->split_join);
   if (c->kws) (void)hipFree(c->kws);
+  if (c->kinst) (void)hipFree(c->kinst);
   if (c->plan_scratch) (void)hipFree(c->plan_scratch);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   if (c->last_ev) (void)hipEventDestroy(c->last_ev);
@@ -453,13 +473,18 @@ const char* hmpc_kernel_name(hmpc_ctx* c) {
       return "hmpc::cas_kernel";
     case hmpc::Kernel::Riccati:
       // (template arguments as rocprofv3 demangles them: variant, occupancy,
-      // compile-time horizon and capacity, 0 = runtime)
+      // compile-time horizon and capacity, 0 = runtime, part; the one-wave
+      // horizons run the factorisation kernel first -- for batches within its
+      // buffer bound, hmpc_ric.hip ric_kinst_stride)
       if (hmpc::ric_occ(c->N) == 2) {
-        if (hmpc::ric_static_n(c->N) == 20) return v3 ? "hmpc::ric_kernel<3, 2, 20, 38>" : "hmpc::ric_kernel<2, 2, 20, 38>";
-        return v3 ? "hmpc::ric_kernel<3, 2, 0, 0>" : "hmpc::ric_kernel<2, 2, 0, 0>";
+        if (hmpc::ric_static_n(c->N) == 20) return v3 ? "hmpc::ric_kernel<3, 2, 20, 38, 0>" : "hmpc::ric_kernel<2, 2, 20, 38, 0>";
+        return v3 ? "hmpc::ric_kernel<3, 2, 0, 0, 0>" : "hmpc::ric_kernel<2, 2, 0, 0, 0>";
       }
-      if (hmpc::ric_static_n(c->N) == 60) return v3 ? "hmpc::ric_kernel<3, 1, 60, 47>" : "hmpc::ric_kernel<2, 1, 60, 47>";
-      return v3 ? "hmpc::ric_kernel<3, 1, 0, 0>" : "hmpc::ric_kernel<2, 1, 0, 0>";
+      if (hmpc::ric_static_n(c->N) == 60)
+        return v3 ? "hmpc::ric_factor_kernel<3, 60, 47> + hmpc::ric_kernel<3, 1, 60, 47, 2>"
+                  : "hmpc::ric_factor_kernel<2, 60, 47> + hmpc::ric_kernel<2, 1, 60, 47, 2>";
+      return v3 ? "hmpc::ric_factor_kernel<3, 0, 0> + hmpc::ric_kernel<3, 1, 0, 0, 2>"
+                : "hmpc::ric_factor_kernel<2, 0, 0> + hmpc::ric_kernel<2, 1, 0, 0, 2>";
     case hmpc::Kernel::Wide:
       if (c->precision == HMPC_PREC_F32 || c->precision == HMPC_PREC_F32_GENERIC)
         return v3 ? "hmpc::wide_kernel<3, float>" : "hmpc::wide_kernel<2, float>";

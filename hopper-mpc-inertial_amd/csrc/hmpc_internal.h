@@ -63,6 +63,11 @@ struct SolveArgs {
   int ric_groups;
   double* kws;
   int64_t kws_stride;
+  // the Riccati factorisation kernel's output (ric_kinst_stride): K / Dinv and
+  // a pivot flag per instance, kinst_stride doubles each; nullptr = the solve
+  // kernel factorises in its own slot
+  double* kinst;
+  int64_t kinst_stride;
   // Dense split launch (hmpc_kernels.hip, objects built with HMPC_CMP_NV):
   // [compacted count | full count] (zero at the launch, zeroed again by the
   // overflow pass at its end) and the two class lists [2][B]; nullptr = one
@@ -109,6 +114,9 @@ size_t ric_lds_bytes(int N, int qcap);
 int64_t ric_kws_stride(int N);   // per-workgroup K / Dinv workspace (doubles)
 int64_t ric_rws_stride(int N);   // per-workgroup overflow block: R (6N capacity) + workspace
 int ric_groups(int variant, int N);   // resident workgroups of the main Riccati kernel
+// per-instance K / Dinv block of the Riccati factorisation kernel, doubles
+// (0: the factorisation stays in the solve kernel)
+int64_t ric_kinst_stride(int N, int64_t B);
 // stance-count buckets of the Riccati kernel's longest-first work queue at
 // horizon N (0: plain index order); their lists take buckets x B ints
 int ric_lpt_buckets(int N);

@@ -54,7 +54,8 @@ constexpr int kMRK = 4;                         // right-hand sides per sweep pa
 // (R in LDS only when r_lds).
 struct RicLay {
   int XIN, CC, CS, BW, ZB, ZN, ZD, MISC, VV, SV, NB, ZV, MU, UA, ACT, CB, SD, RM, U0, total;
-  __host__ __device__ RicLay(int N, int cap, bool r_lds) {
+  // fac: the factorisation kernel's layout (stage data, then the union)
+  __host__ __device__ RicLay(int N, int cap, bool r_lds, bool fac = false) {
     const int NV = 6 * N;
     auto up2 = [](int x) { return (x + 1) & ~1; };   // 16-B alignment of every array
     int o = 0;
@@ -62,6 +63,11 @@ struct RicLay {
     CC = o; o = up2(o + N);
     CS = o; o += 2 * N;
     BW = o; o += 18 * N;
+    if (fac) {
+      ZB = ZN = ZD = MISC = VV = SV = NB = ZV = MU = UA = ACT = CB = SD = U0 = RM = o;
+      total = o + (568 > 12 * N ? 568 : 12 * N);
+      return;
+    }
     ZB = o; o = up2(o + N + 1);   // free-response heights z_k, k = 0..N
     ZN = o; o = up2(o + N);       // |n| of the z row of stage k
     ZD = o; o = up2(o + N);       // z-row dots of s = H^-1 n_p
@@ -90,6 +96,9 @@ constexpr int PS_OFF = 0, P2_OFF = 144, TS_OFF = 288, FS_OFF = 360, GS_OFF = 432
 // lower; G_k^-1 = Dinv_k' Dinv_k) of every stage -- written by the
 // factorisation, read by every sweep
 __host__ __device__ inline int64_t ric_kws_doubles(int N) { return ((93 * (int64_t)N) + 15) & ~(int64_t)15; }
+// the factorisation kernel's per-instance output (ric_kinst_stride): K / Dinv
+// of every stage, then a flag (nonzero: a non-positive pivot)
+__host__ __device__ inline int64_t ric_kinst_doubles(int N) { return ((93 * (int64_t)N + 1) + 15) & ~(int64_t)15; }
 
 __device__ __forceinline__ int loff(int r) { return (r * (r + 1)) >> 1; }
 
@@ -164,7 +173,10 @@ constexpr double kZcRel = 1e-3;   // the z-fallback threshold
 // NC, CAPC > 0: the horizon and the R capacity as compile-time constants
 // (every LDS offset and loop bound folds; the runtime-N instantiation serves
 // any other horizon)
-template <int VAR, int ENT, int RING, bool ZC, int NC = 0, int CAPC = 0>
+// PART: 0 the whole solve; 1 phases 0 and 2 only (the
+// factorisation kernel: K / Dinv and the pivot flag to kw); 2 every phase but
+// the factorisation, whose K / Dinv and flag kw already holds
+template <int VAR, int ENT, int RING, bool ZC, int NC = 0, int CAPC = 0, int PART = 0>
 __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, double* sm, double* Rm,
                           const int cap_, double* kw, double* scw) {
   // lane and N through volatile asm: made afresh for every instance, so the
@@ -176,7 +188,7 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
   if constexpr (NC > 0) N = NC;
   else asm volatile("s_mov_b32 %0, %1" : "=s"(N) : "s"(N_));
   const int cap = CAPC > 0 ? CAPC : cap_;
-  const RicLay L(N, cap, false);
+  const RicLay L(N, cap, false, PART == 1);
   const int NV = 6 * N;
   const double dt = a.dt, dtm = dt / a.m;
   const double zc = dt * dtm;   // coefficient scale of fz_j in z_k
@@ -242,7 +254,7 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
   // lane r < 12 holds component r.  d_t = kf Q (xbar_t - r_{t-1}) goes to
   // ZV..MU (12 N, free until phase 3), x_ref is staged in the union; the gradient h = 2 Gamma' W (xbar - r) - 2 V ubar goes to
   // NB as -h (the right-hand side of the unconstrained optimum).
-  {
+  if constexpr (PART != 1) {
     double* dd = zv;
     double xr = lane < 12 ? xin[lane] : 0.0;
     const double qr = qdiag(lane);
@@ -295,7 +307,9 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
   // Work items are laid over the 64 lanes with a second item per lane for
   // the overhang, both in one unrolled body (their LDS latencies overlap).
   int status = ST_SOLVED;
-  {
+  if constexpr (PART == 2) {   // factorised by the factorisation kernel
+    if (kw[93 * N] != 0.0) status = ST_NUMERICAL;
+  } else {
     double* Pc = un + PS_OFF;   // P_{k+1}, 12 x 12 full
     double* Pn = un + P2_OFF;   // P_k
     double* T = un + TS_OFF;    // P B, 12 x 6
@@ -510,6 +524,10 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
       RS_ACC(14, t_fd);
     }
     if (nbad != 0.0) status = ST_NUMERICAL;
+  }
+  if constexpr (PART == 1) {   // the factorisation kernel: the pivot flag, then done
+    if (lane == 0) kw[93 * N] = status == ST_SOLVED ? 0.0 : 1.0;
+    return;
   }
   gsync();   // K, Dinv (global) visible to every lane of the workgroup
 
@@ -1402,7 +1420,9 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
 constexpr int kRing1Wave = 3;   // (4-6 slots measured slower)
 // ... and at 2 waves/SIMD (register budget 256)
 constexpr int kRing2Wave = 2;
-template <int VAR, int OCC, int NC = 0, int CAPC = 0>
+// PART 2: the factorisation kernel has run, K / Dinv per
+// instance in a.kinst; the workgroup's slot keeps only the cached columns.
+template <int VAR, int OCC, int NC = 0, int CAPC = 0, int PART = 0>
 __global__ void __launch_bounds__(RT) __attribute__((amdgpu_waves_per_eu(OCC, OCC))) ric_kernel(SolveArgs a, int N, int cap) {
   extern __shared__ __attribute__((aligned(16))) double ric_sm[];
   if constexpr (NC > 0) { N = NC; cap = CAPC; }
@@ -1424,10 +1444,27 @@ __global__ void __launch_bounds__(RT) __attribute__((amdgpu_waves_per_eu(OCC, OC
     }
     b = __builtin_amdgcn_readfirstlane(b);
     if (b >= a.B) break;
-    ric_solve<VAR, 1, OCC == 2 ? kRing2Wave : kRing1Wave, true, NC, CAPC>(a, N, (int64_t)b, ric_sm, ric_sm + L.RM, cap, kw,
-                                                         kw + ric_kws_doubles(N));
+    double* kwi = PART == 2 ? a.kinst + (int64_t)b * a.kinst_stride : kw;
+    ric_solve<VAR, 1, OCC == 2 ? kRing2Wave : kRing1Wave, true, NC, CAPC, PART>(a, N, (int64_t)b, ric_sm, ric_sm + L.RM,
+                                                                               cap, kwi, kw + ric_kws_doubles(N));
     __syncthreads();
   }
+}
+
+// The factorisation kernel (ric_kinst_stride): one workgroup per instance,
+// phases 0 and 2 of ric_solve into the instance's K / Dinv block of a.kinst.
+// Few registers and 21 N + max(568, 12 N) doubles of LDS, so several waves
+// per SIMD share the factorisation's dependent chains, which the
+// one-instance-per-wave solve kernel leaves latency-bound.
+// 3 waves / SIMD: 162 VGPRs, no spill (4: 128 B/lane of spill, -10 % at
+// configs[3])
+template <int VAR, int NC = 0, int CAPC = 0>
+__global__ void __launch_bounds__(RT) __attribute__((amdgpu_waves_per_eu(3)))
+ric_factor_kernel(SolveArgs a, int N, int cap) {
+  extern __shared__ __attribute__((aligned(16))) double ric_sm[];
+  if constexpr (NC > 0) { N = NC; cap = CAPC; }
+  const int64_t b = blockIdx.x;
+  ric_solve<VAR, 1, kRing2Wave, true, NC, CAPC, 1>(a, N, b, ric_sm, nullptr, cap, a.kinst + b * a.kinst_stride, nullptr);
 }
 
 // the overflow pass: instances listed in a.ovf_list, capacity 6N, R and the
@@ -1576,9 +1613,29 @@ bool ric_launch_k(K kern, int N, int cap, const SolveArgs& a, hipStream_t s, int
 // were built for: +7 % at N = 60 (B = 4096), +1.4 % at N = 20 (B = 262144;
 // 12 B/lane of scratch at the 2-wave 256-VGPR cap since the round-2 register
 // savings -- it lost 6 % when it spilled more)
+// the factorisation kernel, one workgroup per instance
+template <typename K>
+bool ric_launch_fac(K kern, int N, int cap, const SolveArgs& a, hipStream_t s) {
+  const size_t lds = (size_t)RicLay(N, cap, false, true).total * sizeof(double);
+  if (!set_lds(kern, lds)) return false;
+  hipLaunchKernelGGL(kern, dim3((unsigned)a.B), dim3(RT), lds, s, a, N, cap);
+  return true;
+}
 template <int VAR, int OCC>
 bool ric_launch(int N, const SolveArgs& a, hipStream_t s, int* per) {
   const int cap = ric_qcap(N);
+  if (a.kinst && !per) {   // factorisation kernel, then the solve kernel without phase 2
+    if constexpr (OCC == 1) {
+      if (ric_static_n(N) == 60)
+        return ric_launch_fac(ric_factor_kernel<VAR, 60, 47>, N, cap, a, s) &&
+               ric_launch_k(ric_kernel<VAR, OCC, 60, 47, 2>, N, cap, a, s, per);
+    } else {
+      if (ric_static_n(N) == 20)
+        return ric_launch_fac(ric_factor_kernel<VAR, 20, 38>, N, cap, a, s) &&
+               ric_launch_k(ric_kernel<VAR, OCC, 20, 38, 2>, N, cap, a, s, per);
+    }
+    return ric_launch_fac(ric_factor_kernel<VAR>, N, cap, a, s) && ric_launch_k(ric_kernel<VAR, OCC, 0, 0, 2>, N, cap, a, s, per);
+  }
   if constexpr (OCC == 1) {
     if (ric_static_n(N) == 60) return ric_launch_k(ric_kernel<VAR, OCC, 60, 47>, N, cap, a, s, per);
   } else {
@@ -1600,6 +1657,20 @@ int ric_groups(int variant, int N) {
   SolveArgs none{};
   if (!ric_launch_any(variant, N, none, nullptr, &per) || per < 1) per = 1;
   return cus * per;
+}
+
+// The separate factorisation kernel pays where the solve kernel runs one
+// wave per SIMD (LDS-bound horizons, N > 24): there the factorisation's
+// chains otherwise run alone on their SIMD.  Interleaved A/B
+// (profiles/r04_ab.json r04l): N = 60 B = 4096 1.475 -> 1.552 M solves/s;
+// at 2 waves / SIMD it gains 1.3 % at configs[3] for a 3.9 GB buffer and
+// loses 7.7 % at B = 16384, so N <= 24 keeps the fused kernel.  Bounded to
+// kKinstBytes of per-instance blocks.
+constexpr int64_t kKinstBytes = (int64_t)4 << 30;
+int64_t ric_kinst_stride(int N, int64_t B) {
+  if (ric_occ(N) != 1) return 0;
+  const int64_t s = ric_kinst_doubles(N);
+  return B * s * (int64_t)sizeof(double) <= kKinstBytes ? s : 0;
 }
 
 int ric_lpt_buckets(int N) {

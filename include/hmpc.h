@@ -260,7 +260,8 @@ int hmpc_set_refinement(hmpc_ctx* ctx, int corrections);
 int hmpc_set_order(hmpc_ctx* ctx, int order);
 
 /* Name of the solve kernel this context's (variant, N, precision) runs on,
-   as rocprofv3 demangles it, e.g. "hmpc::ric_kernel<3, 2, 0, 0>"; a split launch names
+   as rocprofv3 demangles it, e.g. "hmpc::ric_kernel<3, 2, 0, 0, 0>" (the Riccati
+   horizons above 24 run "hmpc::ric_factor_kernel<...> + hmpc::ric_kernel<..., 2>"); a split launch names
    every class kernel, "hmpc::solve_kernel<3, 10, double, 48, 13> + hmpc::solve_kernel<3, 10,
    double, 0, 0>" (the narrowest first; 2f's full class is the 5N-wide
    "hmpc::solve_kernel<2, 10, double, 50, 20>").  Static string, "" when none.  For

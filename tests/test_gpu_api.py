@@ -65,9 +65,9 @@ def test_bad_tensors_raise(hm):
 
 def test_kernel_names(hm):
     assert make(hm, 10).kernel_name == DENSE10_3F
-    assert make(hm, 20).kernel_name == 'hmpc::ric_kernel<3, 2, 20, 38>'   # 2 waves / SIMD
-    assert make(hm, 60).kernel_name == 'hmpc::ric_kernel<3, 1, 60, 47>'   # compile-time N = 60
-    assert make(hm, 10, 'f64_riccati').kernel_name == 'hmpc::ric_kernel<3, 2, 0, 0>'
+    assert make(hm, 20).kernel_name == 'hmpc::ric_kernel<3, 2, 20, 38, 0>'   # 2 waves / SIMD
+    assert make(hm, 60).kernel_name == 'hmpc::ric_factor_kernel<3, 60, 47> + hmpc::ric_kernel<3, 1, 60, 47, 2>'   # compile-time N = 60
+    assert make(hm, 10, 'f64_riccati').kernel_name == 'hmpc::ric_kernel<3, 2, 0, 0, 0>'
     assert make(hm, 20, 'f64_dense').kernel_name == 'hmpc::solve_kernel<3, 20, double, 0, 0>'
     assert make(hm, 10, 'f64_generic').kernel_name == 'hmpc::wide_kernel<3, double>'
     assert make(hm, 10, 'f32').kernel_name == ('hmpc::solve_kernel<3, 10, float, 48, 13> + '

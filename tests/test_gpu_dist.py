@@ -37,7 +37,7 @@ def _free_port():
 
 # name -> (horizon, --curve, global batch or 0 = PER_RANK per rank, kernel)
 WORKLOADS = {'cfg2_weak': (N, True, 0, DENSE10_3F),
-             'cfg3_strong': (20, False, 4097, 'hmpc::ric_kernel<3, 2, 20, 38>')}
+             'cfg3_strong': (20, False, 4097, 'hmpc::ric_kernel<3, 2, 20, 38, 0>')}
 
 
 def _ctx(hmpc, n=N):

@@ -82,7 +82,7 @@ def solve_both(hm, N, inst, precision):
 
 
 @pytest.mark.parametrize('precision,kernel', [('f64', DENSE10_3F),
-                                             ('f64_riccati', 'hmpc::ric_kernel<3, 2, 0, 0>')])
+                                             ('f64_riccati', 'hmpc::ric_kernel<3, 2, 0, 0, 0>')])
 def test_overflow_n10(hm, precision, kernel):
     N, B = 10, 48
     inst = adversarial(B, N, 2, 50.0, 8.0, mu=0.2)   # optimal active sets up to 55 of 60
@@ -101,7 +101,7 @@ def test_overflow_n60(hm):
     N, B = 60, 24
     inst = adversarial(B, N, 2, 12.0, 2.0)
     gpu, ref, k, cap = solve_both(hm, N, inst, 'f64')
-    assert k == 'hmpc::ric_kernel<3, 1, 60, 47>'
+    assert k == 'hmpc::ric_factor_kernel<3, 60, 47> + hmpc::ric_kernel<3, 1, 60, 47, 2>'
     assert (ref['status'] == 0).all()
     assert np.array_equal(gpu['status'], ref['status'])
     assert np.abs(gpu['u'] - ref['u']).max() <= U_TOL

@@ -26,11 +26,11 @@ def hm():
 
 
 @pytest.mark.parametrize('variant,N,B,curve,kernel', [
-    ('3f', 13, 2048, True, 'hmpc::ric_kernel<3, 2, 0, 0>'),
-    ('3f', 20, 4096, False, 'hmpc::ric_kernel<3, 2, 20, 38>'),
-    ('2f', 20, 2048, True, 'hmpc::ric_kernel<2, 2, 20, 38>'),
-    ('3f', 40, 1024, True, 'hmpc::ric_kernel<3, 1, 0, 0>'),
-    ('3f', 60, 1024, False, 'hmpc::ric_kernel<3, 1, 60, 47>'),
+    ('3f', 13, 2048, True, 'hmpc::ric_kernel<3, 2, 0, 0, 0>'),
+    ('3f', 20, 4096, False, 'hmpc::ric_kernel<3, 2, 20, 38, 0>'),
+    ('2f', 20, 2048, True, 'hmpc::ric_kernel<2, 2, 20, 38, 0>'),
+    ('3f', 40, 1024, True, 'hmpc::ric_factor_kernel<3, 0, 0> + hmpc::ric_kernel<3, 1, 0, 0, 2>'),
+    ('3f', 60, 1024, False, 'hmpc::ric_factor_kernel<3, 60, 47> + hmpc::ric_kernel<3, 1, 60, 47, 2>'),
 ])
 def test_riccati_stress_vs_port(hm, variant, N, B, curve, kernel):
     import hmpc_plan

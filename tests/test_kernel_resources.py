@@ -77,8 +77,12 @@ def solve(v, n, t, nvm, q):
     return f'_ZN4hmpc12_GLOBAL__N_112solve_kernelILi{v}ELi{n}E{t}Li{nvm}ELi{q}EEEvNS_9SolveArgsE'
 
 
-def ric(v, occ, n, cap):
-    return f'_ZN4hmpc12_GLOBAL__N_110ric_kernelILi{v}ELi{occ}ELi{n}ELi{cap}EEEvNS_9SolveArgsEii'
+def ric(v, occ, n, cap, part=0):
+    return f'_ZN4hmpc12_GLOBAL__N_110ric_kernelILi{v}ELi{occ}ELi{n}ELi{cap}ELi{part}EEEvNS_9SolveArgsEii'
+
+
+def ric_factor(v, n, cap):
+    return f'_ZN4hmpc12_GLOBAL__N_117ric_factor_kernelILi{v}ELi{n}ELi{cap}EEEvNS_9SolveArgsEii'
 
 
 @pytest.mark.parametrize('v', [3, 2])
@@ -115,7 +119,11 @@ def test_dense_fp32_builds(kernels):
 
 
 def test_riccati_budgets(kernels):
-    (n60,) = kernels[ric(3, 1, 60, 47)]   # the Runner's horizon, 1 wave / SIMD
+    # the Runner's horizon: the factorisation kernel (3 waves / SIMD, no
+    # spill), then the solve kernel without phase 2 (1 wave / SIMD)
+    (fac,) = kernels[ric_factor(3, 60, 47)]
+    assert fac['.vgpr_count'] <= 168 and fac['.private_segment_fixed_size'] == 0
+    (n60,) = kernels[ric(3, 1, 60, 47, 2)]
     assert n60['.private_segment_fixed_size'] == 0
     assert n60['.vgpr_count'] + n60['.agpr_count'] <= 512
     (n20,) = kernels[ric(3, 2, 20, 38)]   # configs[3], 2 waves / SIMD
