@@ -260,19 +260,21 @@ int prepare_ric(hmpc_ctx* c, int64_t B, hmpc::SolveArgs& a) {
     a.kws = c->kws;
     a.kws_stride = hmpc::ric_kws_stride(c->N);
     a.ric_groups = c->ric_groups;
-    // the factorisation kernel's per-instance K / Dinv blocks
+    // the factorisation kernel's per-instance K / Dinv blocks (a speed-up
+    // only: without the memory the solve kernel factorises itself)
     const int64_t ks = hmpc::ric_kinst_stride(c->N, B);
     if (ks > 0) {
       if (B > c->kinst_cap) {
         if (c->kinst) (void)hipFree(c->kinst);
         c->kinst = nullptr;
         c->kinst_cap = 0;
-        hipError_t e = hipMalloc(&c->kinst, sizeof(double) * (size_t)ks * (size_t)B);
-        if (e != hipSuccess) { c->err = "Riccati factorisation hipMalloc"; return HMPC_ERR_NOMEM; }
-        c->kinst_cap = B;
+        if (hipMalloc(&c->kinst, sizeof(double) * (size_t)ks * (size_t)B) == hipSuccess) c->kinst_cap = B;
+        else { c->kinst = nullptr; (void)hipGetLastError(); }
       }
-      a.kinst = c->kinst;
-      a.kinst_stride = ks;
+      if (c->kinst) {
+        a.kinst = c->kinst;
+        a.kinst_stride = ks;
+      }
     }
     // the longest-first work queue: stance-count buckets (<= 13 counters in
     // the overflow header), lists of B entries each
