@@ -5,7 +5,11 @@ Build:  OUT=libhmpc_stamps.so BDIR=build_stamps HORIZONS=10 \\
 Run:    HMPC_LIB=hopper-mpc-inertial_amd/libhmpc_stamps.so \\
         python tools/ric_stamps.py variant N B [mu] [curve]
 The stamped kernel writes accumulated s_memtime cycles over each instance's
-x* row (slots in hmpc_ric.hip: RS_ACC).
+x* row (slots in hmpc_ric.hip: RS_ACC).  Add -DHMPC_RIC_GROUPS_PER_CU=4 to the
+build to run the persistent grid at one workgroup per SIMD (round 4: 378 k vs
+410 k cycles per N = 20 instance at one vs two waves per SIMD).  Horizons
+above 24 factorise in a kernel of their own (ric_factor_kernel), whose phase
+is not stamped.
 """
 import json
 import os
