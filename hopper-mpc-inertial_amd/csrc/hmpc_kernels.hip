@@ -2000,6 +2000,14 @@ __global__ void __launch_bounds__(kClsT) classify_kernel(SolveArgs a) {
 #ifndef HMPC_LAUNCH_SUFFIX
 #define HMPC_LAUNCH_SUFFIX
 #endif
+// diagnostic builds (tools/phase_stamps.py): dynamic LDS added to the class
+// launches to hold residency down (16 / 24 KB: one wave per SIMD)
+#ifndef HMPC_DIAG_LDS_FULL
+#define HMPC_DIAG_LDS_FULL 0
+#endif
+#ifndef HMPC_DIAG_LDS_CMP
+#define HMPC_DIAG_LDS_CMP 0
+#endif
 #if defined(HMPC_CMP_NV) && HMPC_CMP_NV > 0
 // the split's compacted kernel launches from a translation unit of its own
 // (-DHMPC_CMP_ONLY): the objects build in parallel
@@ -2019,15 +2027,17 @@ bool HMPC_FULL2F_LAUNCH(const SolveArgs& a, hipStream_t s);
 #ifdef HMPC_CMP_ONLY
 bool HMPC_CMP_LAUNCH(int variant, const SolveArgs& a, hipStream_t s) {
   if (variant == 3)
-    hipLaunchKernelGGL((solve_kernel<3, HMPC_INST_N, real, HMPC_CMP_NV, HMPC_CMP_Q>), dim3((unsigned)a.B), dim3(64), 0, s, a);
+    hipLaunchKernelGGL((solve_kernel<3, HMPC_INST_N, real, HMPC_CMP_NV, HMPC_CMP_Q>), dim3((unsigned)a.B), dim3(64),
+                       HMPC_DIAG_LDS_CMP, s, a);
   else
-    hipLaunchKernelGGL((solve_kernel<2, HMPC_INST_N, real, HMPC_CMP_NV, HMPC_CMP_Q>), dim3((unsigned)a.B), dim3(64), 0, s, a);
+    hipLaunchKernelGGL((solve_kernel<2, HMPC_INST_N, real, HMPC_CMP_NV, HMPC_CMP_Q>), dim3((unsigned)a.B), dim3(64),
+                       HMPC_DIAG_LDS_CMP, s, a);
   return true;
 }
 #ifdef HMPC_FULL2F_NV
 bool HMPC_FULL2F_LAUNCH(const SolveArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL((solve_kernel<2, HMPC_INST_N, real, HMPC_FULL2F_NV, HMPC_FULL2F_Q>), dim3((unsigned)a.B), dim3(64), 0,
-                     s, a);
+  hipLaunchKernelGGL((solve_kernel<2, HMPC_INST_N, real, HMPC_FULL2F_NV, HMPC_FULL2F_Q>), dim3((unsigned)a.B), dim3(64),
+                     HMPC_DIAG_LDS_FULL, s, a);
   return true;
 }
 #endif
@@ -2073,7 +2083,7 @@ bool HMPC_CAT(HMPC_CAT(launch_solve_n, HMPC_INST_N), HMPC_LAUNCH_SUFFIX)(int var
       if (hipStreamWaitEvent(a.split_stream, a.split_fork, 0) != hipSuccess) return false;
       s2 = a.split_stream;
     }
-    if (variant == 3) hipLaunchKernelGGL((solve_kernel<3, N, real>), dim3((unsigned)a.B), dim3(NT), 0, s, af);
+    if (variant == 3) hipLaunchKernelGGL((solve_kernel<3, N, real>), dim3((unsigned)a.B), dim3(NT), HMPC_DIAG_LDS_FULL, s, af);
 #ifdef HMPC_FULL2F_NV
     else HMPC_FULL2F_LAUNCH(af, s);
 #else
