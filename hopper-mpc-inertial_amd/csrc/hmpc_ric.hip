@@ -217,7 +217,7 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
   constexpr bool kMRL = kMR;
   static_assert(6 * kRicNmax <= 568, "an MRHS column must fit the union's Riccati scratch");
   // MRHS candidate columns: after the cached active columns S (cap x NV)
-  [[maybe_unused]] double* gcache = kMR ? scw + (int64_t)cap * NV : nullptr;
+  [[maybe_unused]] double* gcache = kMR && scw ? scw + (int64_t)cap * NV : nullptr;   // (none in the factorisation kernel)
 
 #ifdef HMPC_STAMPS
   long long rst_[16] = {0};
