@@ -101,3 +101,39 @@ def test_n60_batch_statuses_equal_port(hm):
     assert np.abs(gpu['u'][ok] - ref['u'][ok]).max() <= U_TOL
     assert np.abs(gpu['x'][ok] - ref['x'][ok]).max() <= U_TOL
     assert (np.abs(gpu['obj'][ok] - ref['obj'][ok]) / np.abs(ref['obj'][ok])).max() <= 1e-8
+
+
+def test_fused_fallback_equals_factorisation_kernel():
+    """Horizons above 24 factorise in a kernel of their own when the
+    per-instance K / Dinv blocks fit 4 GB (hmpc_ric.hip ric_kinst_stride);
+    a larger batch (here 100 000 x N = 60: 4.5 GB) falls back to the fused
+    solve kernel.  Both run the same phase-2 arithmetic, so the instances
+    they share come out bit for bit equal, and equal to the C port."""
+    import numpy as np
+    import torch
+    if not torch.cuda.is_available():
+        pytest.fail('GPU tests need an MI355X (torch.cuda.is_available() is False)')
+    import hmpc
+    import hmpc_plan
+    from oracle import port
+    N, B, n = 60, 100_000, 48
+    c = hmpc_plan.runner_constants()
+    inst = hmpc_plan.sample_instances(B, N, curve=False, seed=61)
+    keys = ('x_in', 'x_lin', 'x_ref', 'pf', 'C', 'mu')
+
+    def run(b):
+        cx = hmpc.Context('3f', N, t=c['t'], m=c['m'], g=c['g'], mu=1.0, Jinv=c['Jinv'], rh=c['rh'])
+        d = {k: torch.from_numpy(np.ascontiguousarray(inst[k][:b])).cuda() for k in keys}
+        out = cx.solve_device(d['x_in'], d['x_lin'], d['x_ref'], d['pf'], d['C'], mu=d['mu'])
+        torch.cuda.synchronize()
+        r = {k: out[k][:n].cpu().numpy() for k in ('u', 'x', 'obj', 'status')}
+        cx.close()
+        return r
+
+    big, small = run(B), run(n)   # fused kernel / factorisation kernel + solve kernel
+    for k in big:
+        assert np.array_equal(big[k], small[k]), k
+    ref = port.solve_batch('3f', N, *(inst[k][:n] for k in keys[:5]), mu=inst['mu'][:n], nthreads=16)
+    assert np.array_equal(big['status'], ref['status'])
+    ok = ref['status'] == 0
+    assert np.abs(big['u'][ok] - ref['u'][ok]).max() <= 1e-6
