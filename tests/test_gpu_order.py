@@ -90,3 +90,28 @@ def test_set_order_rejects_unknown(hm):
     with pytest.raises(hm.HmpcError):
         cx._check(cx._lib.hmpc_set_order(cx._h, 7), 'hmpc_set_order')
     cx.close()
+
+
+@pytest.mark.parametrize('N', [10, 20, 40])
+def test_ragged_small_batches(hm, N):
+    """Batches of 1, 2, 3, 63, 65 and 1025 instances through every kernel
+    path small batches take: the dense split with longest-first buckets
+    (N = 10; a class may be empty), the two-wave Riccati queue (N = 20), the
+    factorisation kernel + one-wave Riccati queue (N = 40).  Each instance
+    must come out as in one large batch, bit for bit, and match the port."""
+    import hmpc_plan
+    from oracle import port
+    inst = hmpc_plan.sample_instances(1025, N, curve=True, seed=300 + N)
+    keys = ('x_in', 'x_lin', 'x_ref', 'pf', 'C')
+    cx = context(hm, '3f', N)
+    whole = cx.solve_host(*(inst[k] for k in keys), mu=inst['mu'])
+    for b in (1, 2, 3, 63, 65):
+        part = cx.solve_host(*(inst[k][:b] for k in keys), mu=inst['mu'][:b])
+        for k in part:
+            assert np.array_equal(part[k], whole[k][:b]), (b, k)
+    cx.close()
+    n = 65
+    ref = port.solve_batch('3f', N, *(inst[k][:n] for k in keys), mu=inst['mu'][:n], nthreads=16)
+    assert np.array_equal(whole['status'][:n], ref['status'])
+    ok = ref['status'] == 0
+    assert np.abs(whole['u'][:n][ok] - ref['u'][ok]).max() <= 1e-6
