@@ -30,9 +30,25 @@ cmp_flags() {   # horizon [list]
     if [ "$cn" = "$1" ]; then echo "-DHMPC_CMP_NV=$cv -DHMPC_CMP_Q=$cq"; fi
   done
 }
+# the split's all-swing class (csrc/hmpc_swing.hip: two instances per wave)
+# per horizon: "N:Q:W" = active-set capacity Q, W waves / SIMD (SWING="" disables)
+SWING=${SWING-"10:13:3"}
+swing_flags() {   # horizon
+  for e in $SWING; do
+    IFS=: read -r sn sq sw <<< "$e"
+    if [ "$sn" = "$1" ]; then echo "-DHMPC_SWING_Q=$sq -DHMPC_SWING_WAVES=$sw"; fi
+  done
+}
 CMPOBJS=""
 for n in $HORIZONS; do
-  $HIPCC $FLAGS -DHMPC_INST_N=$n $(cmp_flags $n) -c ${KSRC:-csrc/hmpc_kernels.hip} -o $BDIR/hmpc_kernels_n$n.o "$@" &
+  SWF=""
+  if [ -n "$(swing_flags $n)" ] && [ -n "$(cmp_flags $n)" ]; then
+    SWF="-DHMPC_SWING=1"
+    $HIPCC $FLAGS -DHMPC_INST_N=$n $(swing_flags $n) -c csrc/hmpc_swing.hip -o $BDIR/hmpc_swing_n$n.o "$@" &
+    pids+=($!)
+    CMPOBJS="$CMPOBJS $BDIR/hmpc_swing_n$n.o"
+  fi
+  $HIPCC $FLAGS -DHMPC_INST_N=$n $(cmp_flags $n) $SWF -c ${KSRC:-csrc/hmpc_kernels.hip} -o $BDIR/hmpc_kernels_n$n.o "$@" &
   pids+=($!)
   if [ -n "$(cmp_flags $n)" ]; then   # the compacted kernel: a translation unit of its own
     $HIPCC $FLAGS -DHMPC_INST_N=$n $(cmp_flags $n) -DHMPC_CMP_ONLY -c ${KSRC:-csrc/hmpc_kernels.hip} -o $BDIR/hmpc_kernels_n${n}_cmp.o "$@" &

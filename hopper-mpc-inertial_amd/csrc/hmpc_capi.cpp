@@ -45,11 +45,15 @@ struct hmpc_ctx {
   // solve whose overflow pass -- which zeroes them at its end -- did not run)
   bool ovf_dirty = true;
   double* rws = nullptr;
-  // dense split launch: the two class lists [2][split_cap], or (longest-first
+  // dense split launch: the three class lists [3][split_cap], or (longest-first
   // order) up to N + 1 stance-count buckets of split_cap entries; the Riccati
   // kernel's longest-first queue uses the same buffer for its buckets
   int32_t* split = nullptr;
   int64_t split_cap = 0;
+  int split_nbuf = 0;   // lists of split_cap entries the buffer holds
+  // the last Riccati solve at a one-wave horizon ran the fused kernel (no
+  // per-instance K / Dinv buffer: beyond its 4 GB bound or out of memory)
+  bool ric_fused = false;
   hipStream_t split_stream = nullptr;   // the compacted class's stream
   hipEvent_t split_fork = nullptr, split_join = nullptr;
   // Riccati kernel: per-workgroup K / Dinv workspace of its resident grid
@@ -166,6 +170,22 @@ bool longest_first(const hmpc_ctx* c, int64_t B) {
   return B <= kDenseLptMaxB;
 }
 
+// The class / bucket lists: nlist lists of B entries (grow-only).
+int ensure_split(hmpc_ctx* c, int64_t B, int nlist, const char* what) {
+  if (B <= c->split_cap && nlist <= c->split_nbuf) return HMPC_OK;
+  if (c->split) (void)hipFree(c->split);
+  c->split = nullptr;
+  const int64_t cap = B > c->split_cap ? B : c->split_cap;
+  const int nb = nlist > c->split_nbuf ? nlist : c->split_nbuf;
+  c->split_cap = 0;
+  c->split_nbuf = 0;
+  hipError_t e = hipMalloc(&c->split, sizeof(int32_t) * (size_t)nb * (size_t)cap);
+  if (e != hipSuccess) { c->split = nullptr; c->err = what; return HMPC_ERR_NOMEM; }
+  c->split_cap = cap;
+  c->split_nbuf = nb;
+  return HMPC_OK;
+}
+
 // Buffers of the dense / Riccati kernels: [overflow count | instance counter |
 // pad | overflow list], the overflow pass's blocks, the Riccati kernel's
 // per-workgroup K / Dinv workspace.
@@ -222,15 +242,10 @@ int prepare_ric(hmpc_ctx* c, int64_t B, hmpc::SolveArgs& a) {
   const bool split = (k == hmpc::Kernel::Dense && hmpc::dense_split_nv(c->N, 0) > 0) ||
                      (k == hmpc::Kernel::DenseF32 && hmpc::dense_split_nv(c->N, 1) > 0);
   if (split && c->N + 1 <= kOvfHeader - 3) {
-    if (B > c->split_cap) {
-      if (c->split) (void)hipFree(c->split);
-      c->split = nullptr;
-      c->split_cap = 0;
-      // (up to N + 1 stance-count buckets of B entries: longest-first order)
-      hipError_t e = hipMalloc(&c->split, sizeof(int32_t) * (size_t)(c->N + 1) * (size_t)B);
-      if (e != hipSuccess) { c->err = "split list hipMalloc"; return HMPC_ERR_NOMEM; }
-      c->split_cap = B;
-    }
+    // (up to N + 1 stance-count buckets of B entries -- longest-first order --
+    // or the three class lists)
+    int rc = ensure_split(c, B, c->N + 1 > 3 ? c->N + 1 : 3, "split list hipMalloc");
+    if (rc != HMPC_OK) return rc;
     if (!c->split_stream) {
       if (hipStreamCreateWithFlags(&c->split_stream, hipStreamNonBlocking) != hipSuccess ||
           hipEventCreateWithFlags(&c->split_fork, hipEventDisableTiming) != hipSuccess ||
@@ -276,19 +291,14 @@ int prepare_ric(hmpc_ctx* c, int64_t B, hmpc::SolveArgs& a) {
         a.kinst_stride = ks;
       }
     }
+    c->ric_fused = hmpc::ric_occ(c->N) == 1 && a.kinst == nullptr;
     // the longest-first work queue: stance-count buckets (<= 13 counters in
     // the overflow header), lists of B entries each
     const int nb = hmpc::ric_lpt_buckets(c->N);
     a.lpt = 0;
     if (longest_first(c, B) && nb > 0 && nb <= kOvfHeader - 3) {
-      if (B > c->split_cap) {
-        if (c->split) (void)hipFree(c->split);
-        c->split = nullptr;
-        c->split_cap = 0;
-        hipError_t e = hipMalloc(&c->split, sizeof(int32_t) * (size_t)(c->N + 1) * (size_t)B);
-        if (e != hipSuccess) { c->err = "work-queue bucket hipMalloc"; return HMPC_ERR_NOMEM; }
-        c->split_cap = B;
-      }
+      int rc = ensure_split(c, B, nb, "work-queue bucket hipMalloc");   // (nb <= 13 lists, not N + 1)
+      if (rc != HMPC_OK) return rc;
       a.split_count = c->ovf + 3;
       a.split_list = c->split;
       a.split_nbkt = nb;
@@ -477,10 +487,15 @@ const char* hmpc_kernel_name(hmpc_ctx* c) {
       // (template arguments as rocprofv3 demangles them: variant, occupancy,
       // compile-time horizon and capacity, 0 = runtime, part; the one-wave
       // horizons run the factorisation kernel first -- for batches within its
-      // buffer bound, hmpc_ric.hip ric_kinst_stride)
+      // buffer bound, hmpc_ric.hip ric_kinst_stride; the fused kernel when
+      // the context's last solve was beyond it)
       if (hmpc::ric_occ(c->N) == 2) {
         if (hmpc::ric_static_n(c->N) == 20) return v3 ? "hmpc::ric_kernel<3, 2, 20, 38, 0>" : "hmpc::ric_kernel<2, 2, 20, 38, 0>";
         return v3 ? "hmpc::ric_kernel<3, 2, 0, 0, 0>" : "hmpc::ric_kernel<2, 2, 0, 0, 0>";
+      }
+      if (c->ric_fused) {   // the last solve's batch was beyond the K / Dinv buffer bound
+        if (hmpc::ric_static_n(c->N) == 60) return v3 ? "hmpc::ric_kernel<3, 1, 60, 47, 0>" : "hmpc::ric_kernel<2, 1, 60, 47, 0>";
+        return v3 ? "hmpc::ric_kernel<3, 1, 0, 0, 0>" : "hmpc::ric_kernel<2, 1, 0, 0, 0>";
       }
       if (hmpc::ric_static_n(c->N) == 60)
         return v3 ? "hmpc::ric_factor_kernel<3, 60, 47> + hmpc::ric_kernel<3, 1, 60, 47, 2>"

@@ -75,6 +75,8 @@ constexpr bool kRefine = kF32 && HMPC_F32_REFINE;
 // the refinement's acceptance: scaled row violations and negative multipliers
 // beyond this send the instance to the fp64 pass
 constexpr double kRefineTol = 1e-9;
+// and the largest last correction accepted as converged
+constexpr double kRefineDu = 4e-6;
 // feasibility tolerance of the slack scan and the relative threshold on
 // |w_perp|^2 for a usable primal direction, per precision
 constexpr real kTolR = kF32 ? real(2e-4) : real(kTol);
@@ -180,6 +182,17 @@ __device__ __forceinline__ void lds_wait(real& a, real& b) {
 template <int CNT>
 __device__ __forceinline__ void lds_wait(real& a) {
   asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(a) : "i"(CNT));
+}
+
+// Drain a ring of hand-counted LDS loads: wait for every load, and keep the
+// ring's registers allocated until then.  The compiler does not know an asm
+// load writes its register asynchronously; a ring slot whose last load is
+// never read (the tail's dummy loads) is dead to it, and a value it placed
+// in that register before the wait would be overwritten when the load lands.
+template <int R>
+__device__ __forceinline__ void lds_drain(real (&r)[R]) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  sfor<0, R>([&](auto ic) __attribute__((always_inline)) { pin(r[decltype(ic)::value]); });
 }
 
 template <int W>
@@ -391,7 +404,7 @@ __device__ __forceinline__ real tri_fwd_lds(real acc, const real* Mc, const real
         lds_ld1(ring[j], addr(sj + kRing1));
       });
     }
-    lds_wait<0>(ring[0]);   // drain the ring (its last loads are dummies)
+    lds_drain(ring);   // the ring's last loads are dummies
   } else {
     static_assert(L::W == 2 && NV > 64, "two-wave sweeps only");
     // Every wave runs the whole sweep on all NV rows (two per lane: lane and
@@ -430,7 +443,8 @@ __device__ __forceinline__ real tri_fwd_lds(real acc, const real* Mc, const real
     for (int s = s0; s < 64; s += RD) steps(s, a0, 0);
 #pragma unroll 1
     for (int s = (s0 > 64 ? s0 : 64); s < SEND; s += RD) steps(s, a1, 64);
-    lds_wait<0>(r0[0], r1[0]);   // drain the ring (its last loads are dummies)
+    lds_drain(r0);   // the ring's last loads are dummies
+    lds_drain(r1);
     acc = tid < 64 ? a0 : a1;
   }
   // lane v's accumulator is final once step v has read it
@@ -470,7 +484,7 @@ __device__ __forceinline__ real tri_bwd(real acc, const real* Mc, const real* ze
         lds_ld1(ring[j], addr(sj - kRing1));
       });
     }
-    lds_wait<0>(ring[0]);   // drain the ring (its last loads are dummies)
+    lds_drain(ring);   // the ring's last loads are dummies
   } else {
     static_assert(L::W == 2 && NV > 64, "two-wave sweeps only");
     // as in tri_fwd_lds: each wave sweeps all rows (lane, lane + 64)
@@ -1695,6 +1709,7 @@ solve_kernel(SolveArgs a) {
       };
       double objl = 0.0;
       const int nref = ka.refine;
+      double lastdu = INFINITY;   // |du| of the last correction (no correction: not converged)
 #pragma unroll 1
       for (int it = 0; it < nref; ++it) {
         rollout(std::false_type{}, nullptr, objl);
@@ -1759,6 +1774,7 @@ solve_kernel(SolveArgs a) {
         });
         const real du = tri_bwd<L>(zq, Lc, zero, dinv, xs, nf);
         u64 += active_lane ? (double)du : 0.0;
+        lastdu = active_lane ? fabs((double)du) : 0.0;
         lam += dlam;
         if (active_lane) dlo[L::DU + fidx] = u64;
         B::sync();
@@ -1781,7 +1797,10 @@ solve_kernel(SolveArgs a) {
           worst = fmin(slack64(id0), slack64(id0 + 1)) * sc;
         }
       }
-      const bool bad = __ballot(worst < -kRefineTol || (tid < qu && lam < -kRefineTol)) != 0;
+      // ... and the convergence: the last correction's size bounds the error
+      // left after it (contraction ~1/20 measured, cond x eps32 <= 0.2 bound:
+      // |du| <= kRefineDu leaves <= 8e-7, inside the fp64 path's 1e-6)
+      const bool bad = __ballot(worst < -kRefineTol || (tid < qu && lam < -kRefineTol) || lastdu > kRefineDu) != 0;
       if (bad) {
         status = ka.ovf_count ? ST_OVERFLOW : ST_NUMERICAL;
       } else {
@@ -1942,12 +1961,14 @@ __global__ void __launch_bounds__(kClsT) classify_buckets_kernel(SolveArgs a) {
   __syncthreads();
   if (in) a.split_list[(int64_t)nst * a.B + base[nst] + wc[w][nst] + __builtin_popcountll(mine & ((1ull << lane) - 1))] = (int32_t)i;
 }
-template <int VAR, int N, int NVM>
+// SW: the all-swing windows (no stance stage) form a third list at
+// split_list[2B..3B), length split_count[2] (hmpc_swing.hip's class)
+template <int VAR, int N, int NVM, bool SW = false>
 __global__ void __launch_bounds__(kClsT) classify_kernel(SolveArgs a) {
   // (one atomic per block and list: per-wave atomics on the two counters
   // serialised at the L2 and made this pass 25 us of a 1.3 ms step)
-  __shared__ int wc[kClsT / 64][2];
-  __shared__ int base[2];
+  __shared__ int wc[kClsT / 64][3];
+  __shared__ int base[3];
   const int64_t i = (int64_t)blockIdx.x * kClsT + threadIdx.x;
   const bool in = i < a.B;
   int nst = 0;
@@ -1957,30 +1978,31 @@ __global__ void __launch_bounds__(kClsT) classify_kernel(SolveArgs a) {
     for (int k = 0; k < N; ++k) nst += c[k] != 0.0 ? 1 : 0;
   }
   const int nf = 3 * N + (VAR == 3 ? 3 : 2) * nst;
-  const bool cmp = in && nf <= NVM, full = in && !cmp;
-  const uint64_t mc = __ballot(cmp), mf = __ballot(full);
+  const bool sw = SW && in && nst == 0;
+  const bool cmp = in && !sw && nf <= NVM, full = in && !sw && !cmp;
+  const uint64_t mc = __ballot(cmp), mf = __ballot(full), ms = __ballot(sw);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   if (lane == 0) {
     wc[w][0] = __builtin_popcountll(mc);
     wc[w][1] = __builtin_popcountll(mf);
+    wc[w][2] = __builtin_popcountll(ms);
   }
   __syncthreads();
-  if (threadIdx.x == 0) {   // exclusive scan of the wave counts, one atomic per list
-    int tc = 0, tf = 0;
+  if (threadIdx.x < (SW ? 3 : 2)) {   // exclusive scan of list t's wave counts, one atomic
+    const int t = threadIdx.x;
+    int tc = 0;
     for (int v = 0; v < kClsT / 64; ++v) {
-      const int c = wc[v][0], f = wc[v][1];
-      wc[v][0] = tc;
-      wc[v][1] = tf;
+      const int c = wc[v][t];
+      wc[v][t] = tc;
       tc += c;
-      tf += f;
     }
-    base[0] = tc ? atomicAdd(a.split_count, tc) : 0;
-    base[1] = tf ? atomicAdd(a.split_count + 1, tf) : 0;
+    base[t] = tc ? atomicAdd(a.split_count + t, tc) : 0;
   }
   __syncthreads();
   const uint64_t lt = (1ull << lane) - 1;
   if (cmp) a.split_list[base[0] + wc[w][0] + __builtin_popcountll(mc & lt)] = (int32_t)i;
   if (full) a.split_list[a.B + base[1] + wc[w][1] + __builtin_popcountll(mf & lt)] = (int32_t)i;
+  if (SW && sw) a.split_list[2 * a.B + base[2] + wc[w][2] + __builtin_popcountll(ms & lt)] = (int32_t)i;
 }
 
 }  // namespace
@@ -2024,6 +2046,13 @@ bool HMPC_CMP_LAUNCH(int variant, const SolveArgs& a, hipStream_t s);
 bool HMPC_FULL2F_LAUNCH(const SolveArgs& a, hipStream_t s);
 #endif
 #endif
+// the all-swing class (hmpc_swing.hip, fp64 objects built with HMPC_SWING):
+// two instances per wave
+#if defined(HMPC_SWING) && HMPC_SWING && !defined(HMPC_CMP_ONLY)
+#define HMPC_SWING_LAUNCH HMPC_CAT(launch_swing_n, HMPC_INST_N)
+bool HMPC_SWING_LAUNCH(const SolveArgs& a, hipStream_t s);
+int HMPC_CAT(swing_qmax_n, HMPC_INST_N)();
+#endif
 #ifdef HMPC_CMP_ONLY
 bool HMPC_CMP_LAUNCH(int variant, const SolveArgs& a, hipStream_t s) {
   if (variant == 3)
@@ -2059,20 +2088,30 @@ bool HMPC_CAT(HMPC_CAT(launch_solve_n, HMPC_INST_N), HMPC_LAUNCH_SUFFIX)(int var
     ac.list_count = a.split_count;
     af.list = a.split_list + a.B;
     af.list_count = a.split_count + 1;
+#ifdef HMPC_SWING_LAUNCH
+    constexpr bool kSw = true;
+#else
+    constexpr bool kSw = false;
+#endif
+    SolveArgs as = af;   // the all-swing class (kSw): list 2, or bucket 0
+    as.list = a.split_list + 2 * a.B;
+    as.list_count = a.split_count + 2;
     if (a.lpt && a.split_nbkt >= N + 1) {
       // bucket ranges: the compacted class takes s <= smax, the full class the rest
       const int smax = (HMPC_CMP_NV - 3 * N) / (variant == 3 ? 3 : 2);
       ac.list = af.list = a.split_list;
       ac.list_count = af.list_count = a.split_count;
-      ac.lpt_lo = 0;
+      ac.lpt_lo = kSw ? 1 : 0;
       ac.lpt_hi = smax;
       af.lpt_lo = smax + 1;
       af.lpt_hi = N;
+      as.list = a.split_list;
+      as.list_count = a.split_count;
       if (variant == 3) hipLaunchKernelGGL((classify_buckets_kernel<3, N>), dim3(cb), dim3(kClsT), 0, s, a);
       else hipLaunchKernelGGL((classify_buckets_kernel<2, N>), dim3(cb), dim3(kClsT), 0, s, a);
     } else {
-      if (variant == 3) hipLaunchKernelGGL((classify_kernel<3, N, HMPC_CMP_NV>), dim3(cb), dim3(kClsT), 0, s, a);
-      else hipLaunchKernelGGL((classify_kernel<2, N, HMPC_CMP_NV>), dim3(cb), dim3(kClsT), 0, s, a);
+      if (variant == 3) hipLaunchKernelGGL((classify_kernel<3, N, HMPC_CMP_NV, kSw>), dim3(cb), dim3(kClsT), 0, s, a);
+      else hipLaunchKernelGGL((classify_kernel<2, N, HMPC_CMP_NV, kSw>), dim3(cb), dim3(kClsT), 0, s, a);
     }
     // the two classes run concurrently: the full kernel on the caller's
     // stream, the compacted one on the split stream, joined back before the
@@ -2088,6 +2127,11 @@ bool HMPC_CAT(HMPC_CAT(launch_solve_n, HMPC_INST_N), HMPC_LAUNCH_SUFFIX)(int var
     else HMPC_FULL2F_LAUNCH(af, s);
 #else
     else hipLaunchKernelGGL((solve_kernel<2, N, real>), dim3((unsigned)a.B), dim3(NT), 0, s, af);
+#endif
+#ifdef HMPC_SWING_LAUNCH
+    HMPC_SWING_LAUNCH(as, s2);
+#else
+    (void)as;
 #endif
     HMPC_CMP_LAUNCH(variant, ac, s2);
     if (s2 != s) {
@@ -2115,27 +2159,36 @@ constexpr int kCapCmp = Lay<HMPC_INST_N, HMPC_CMP_NV, HMPC_CMP_Q>::QMAX;
 constexpr int kCapCmp = 1 << 30;
 #endif
 int HMPC_CAT(HMPC_CAT(qmax_solve_n, HMPC_INST_N), HMPC_LAUNCH_SUFFIX)() {
-  return Lay<HMPC_INST_N>::QMAX < kCapCmp ? Lay<HMPC_INST_N>::QMAX : kCapCmp;
+  int q = Lay<HMPC_INST_N>::QMAX < kCapCmp ? Lay<HMPC_INST_N>::QMAX : kCapCmp;
+#ifdef HMPC_SWING_LAUNCH
+  const int qs = HMPC_CAT(swing_qmax_n, HMPC_INST_N)();
+  q = qs < q ? qs : q;
+#endif
+  return q;
 }
 int HMPC_CAT(HMPC_CAT(split_nv_n, HMPC_INST_N), HMPC_LAUNCH_SUFFIX)() { return HMPC_SPLIT_NV; }
 const char* HMPC_CAT(HMPC_CAT(name_solve_n, HMPC_INST_N), HMPC_LAUNCH_SUFFIX)(int variant) {
   // (the template arguments as rocprofv3 demangles them; split classes:
-  // narrow + compacted + full)
+  // all-swing + compacted + full).  Built once per variant, thread-safely
+  // (function-local statics).
   if (variant != 2 && variant != 3) return "";
-  static std::string names[2];
-  std::string& name = names[variant - 2];
-  if (name.empty()) {
+  auto build = [](int var) {
+    std::string name;
     const char* real_s = HMPC_STR(HMPC_REAL);
     char buf[160];
     auto add = [&](const char* k, int nv, int q) {
-      snprintf(buf, sizeof buf, "%shmpc::%s<%d, %d, %s, %d, %d>", name.empty() ? "" : " + ", k, variant,
+      snprintf(buf, sizeof buf, "%shmpc::%s<%d, %d, %s, %d, %d>", name.empty() ? "" : " + ", k, var,
                HMPC_INST_N, real_s, nv, q);
       name += buf;
     };
 #if defined(HMPC_CMP_NV) && HMPC_CMP_NV > 0
+#ifdef HMPC_SWING_LAUNCH
+    snprintf(buf, sizeof buf, "hmpc::swing_kernel<%d, %d>", HMPC_INST_N, HMPC_CAT(swing_qmax_n, HMPC_INST_N)());
+    name += buf;
+#endif
     add("solve_kernel", HMPC_CMP_NV, HMPC_CMP_Q);
 #ifdef HMPC_FULL2F_NV
-    if (variant == 2) add("solve_kernel", HMPC_FULL2F_NV, HMPC_FULL2F_Q);
+    if (var == 2) add("solve_kernel", HMPC_FULL2F_NV, HMPC_FULL2F_Q);
     else add("solve_kernel", 0, 0);
 #else
     add("solve_kernel", 0, 0);
@@ -2143,8 +2196,10 @@ const char* HMPC_CAT(HMPC_CAT(name_solve_n, HMPC_INST_N), HMPC_LAUNCH_SUFFIX)(in
 #else
     add("solve_kernel", 0, 0);
 #endif
-  }
-  return name.c_str();
+    return name;
+  };
+  static const std::string n2 = build(2), n3 = build(3);
+  return variant == 2 ? n2.c_str() : n3.c_str();
 }
 #endif  // HMPC_CMP_ONLY
 

@@ -1504,27 +1504,36 @@ __global__ void __launch_bounds__(RT) ric_overflow_kernel(SolveArgs a, int N) {
 }
 
 // The longest-first work queue (a.lpt: a few instances per workgroup, where
-// the queue's last round is the tail): one thread per instance counts
-// its stance stages and appends the instance to bucket nst / W (W stages per
+// the queue's last round is the tail): every instance's stance stages are
+// counted and the instance is appended to bucket nst / W (W stages per
 // bucket, nb <= kLptMax buckets at split_list[bucket * B ..], lengths in
 // split_count[bucket], zero at the launch; the overflow pass zeroes them).
 // The kernel then serves the buckets from the most stance stages down.
-constexpr int kLptT = 1024;
-constexpr int kLptMax = 13;   // bucket counters in the overflow header (hmpc_capi.cpp)
+// Each wave counts its 64 instances row by row: lane j < N reads C[i][j], one
+// coalesced row per load and a ballot (round 5; one thread per instance
+// walking its own row was 64 uncoalesced loads per instruction and 50 us per
+// N = 60 step at B = 4096).
+constexpr int kLptT = 256;
+constexpr int kLptMax = 13;
+static_assert(kRicNmax <= 64, "a C row per wave load");   // bucket counters in the overflow header (hmpc_capi.cpp)
 __global__ void __launch_bounds__(kLptT) ric_buckets_kernel(SolveArgs a, int N, int W) {
   __shared__ int wc[kLptT / 64][kLptMax];
   __shared__ int base[kLptMax];
   const int nb = a.split_nbkt;
-  const int64_t i = (int64_t)blockIdx.x * kLptT + threadIdx.x;
-  const bool in = i < a.B;
-  int k = 0;
-  if (in) {
-    const double* c = a.C + i * a.C_bs;
-    int nst = 0;
-    for (int j = 0; j < N; ++j) nst += c[j] != 0.0 ? 1 : 0;
-    k = min(nst / W, nb - 1);
-  }
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t i0 = (int64_t)blockIdx.x * kLptT + 64 * w;   // this wave's 64 instances
+  const int64_t i = i0 + lane;
+  const bool in = i < a.B;
+  int nst = 0;
+#pragma unroll 8
+  for (int r = 0; r < 64; ++r) {
+    const int64_t ir = i0 + r;
+    const bool ok = ir < a.B && lane < N;
+    const double cv = a.C[(ok ? ir * a.C_bs + lane : 0)];
+    const int cnt = __builtin_popcountll(__ballot(ok && cv != 0.0));
+    nst = lane == r ? cnt : nst;
+  }
+  const int k = in ? min(nst / W, nb - 1) : 0;
   uint64_t mine = 0;
   for (int s = 0; s < nb; ++s) {
     const uint64_t m = __ballot(in && k == s);

@@ -9,7 +9,7 @@ GOLDEN = os.path.join(ROOT, 'tests', 'golden')
 # the default build's N = 10 3f dense dispatch: the split's persistent class
 # kernels (compacted nf <= 48, then the full class), as hmpc_kernel_name
 # reports them (build.sh CMP)
-DENSE10_3F = 'hmpc::solve_kernel<3, 10, double, 48, 13> + hmpc::solve_kernel<3, 10, double, 0, 0>'
+DENSE10_3F = 'hmpc::swing_kernel<10, 13> + hmpc::solve_kernel<3, 10, double, 48, 13> + hmpc::solve_kernel<3, 10, double, 0, 0>'
 for p in (PKG, ROOT, os.path.join(ROOT, 'tools')):
     if p not in sys.path:
         sys.path.insert(0, p)

@@ -70,9 +70,12 @@ def test_fp32_dense_bounded(hm, variant, curve, musweep):
 
 def test_fp32_dense_overflow_goes_to_the_fp64_pass(hm):
     """An fp32 instance whose active set outgrows the kernel's 20 is re-solved
-    by the (fp64) overflow pass: solved, and to fp64 accuracy."""
+    by the (fp64) overflow pass: solved, and to fp64 accuracy -- checked on
+    exactly the instances whose optimal active set (counted on the CPU from
+    the port's optimum against the reference-form rows) exceeds 20."""
     import hmpc_plan
     from oracle import port
+    from test_gpu_overflow import active_rows
     N, B = 10, 48
     inst = hmpc_plan.sample_instances(B, N, curve=True, seed=2, mu_sweep=(0.2, 0.2))
     rng = np.random.default_rng(2)
@@ -86,7 +89,10 @@ def test_fp32_dense_overflow_goes_to_the_fp64_pass(hm):
     assert (ref['status'] == 0).all()
     assert (g['status'] == 0).all()
     du = np.abs(g['u'] - ref['u']).max(axis=(1, 2))
-    assert (du <= 1e-6).any()   # the overflowed ones, solved in fp64
+    nact = np.array([active_rows(N, inst, ref, i) for i in range(B)])
+    over = nact > 20   # beyond every fp32 class's capacity (13 compacted, 20 full)
+    assert over.sum() >= 8, nact
+    assert du[over].max() <= 1e-6, (du[over], nact[over])
 
 
 @pytest.mark.parametrize('variant,curve,musweep', [('3f', True, False), ('3f', False, True),
@@ -131,3 +137,20 @@ def test_fp32_refined_contracts(hm, k, bound):
     assert np.array_equal(g['status'], ref['status'])
     ok = ref['status'] == 0
     assert np.abs(g['u'][ok] - ref['u'][ok]).max() <= bound
+
+
+def test_fp32_refined_unconverged_goes_to_fp64(hm):
+    """A refinement that has not converged is not reported as solved (ADVICE
+    r4): with one correction the last step is far above the acceptance bound
+    (kRefineDu), so every instance is re-solved by the fp64 pass -- statuses
+    equal, |du| <= 1e-6 (one correction alone leaves ~2e-2)."""
+    import hmpc_plan
+    from oracle import port
+    N, B = 10, 256
+    inst = hmpc_plan.sample_instances(B, N, curve=True, seed=95)
+    g, _ = solve(hm, 'f32_refined', inst, N, '3f', refine=1)
+    ref = port.solve_batch('3f', N, inst['x_in'], inst['x_lin'], inst['x_ref'], inst['pf'], inst['C'],
+                           mu=inst['mu'], nthreads=16)
+    assert np.array_equal(g['status'], ref['status'])
+    ok = ref['status'] == 0
+    assert np.abs(g['u'][ok] - ref['u'][ok]).max() <= 1e-6
