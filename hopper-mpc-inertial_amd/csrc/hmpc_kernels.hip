@@ -2113,7 +2113,7 @@ bool HMPC_CAT(HMPC_CAT(launch_solve_n, HMPC_INST_N), HMPC_LAUNCH_SUFFIX)(int var
       if (variant == 3) hipLaunchKernelGGL((classify_kernel<3, N, HMPC_CMP_NV, kSw>), dim3(cb), dim3(kClsT), 0, s, a);
       else hipLaunchKernelGGL((classify_kernel<2, N, HMPC_CMP_NV, kSw>), dim3(cb), dim3(kClsT), 0, s, a);
     }
-    // the two classes run concurrently: the full kernel on the caller's
+    // the classes run concurrently: the full kernel on the caller's
     // stream, the compacted one on the split stream, joined back before the
     // overflow pass (one kernel's tail fills with the other's waves)
     hipStream_t s2 = s;
@@ -2122,18 +2122,37 @@ bool HMPC_CAT(HMPC_CAT(launch_solve_n, HMPC_INST_N), HMPC_LAUNCH_SUFFIX)(int var
       if (hipStreamWaitEvent(a.split_stream, a.split_fork, 0) != hipSuccess) return false;
       s2 = a.split_stream;
     }
-    if (variant == 3) hipLaunchKernelGGL((solve_kernel<3, N, real>), dim3((unsigned)a.B), dim3(NT), HMPC_DIAG_LDS_FULL, s, af);
+    // The classes' order on the two streams (interleaved A/B, profiles/r05_ab.json):
+    //   large batches: swing then full on the caller's stream, compacted on the
+    //   split stream -- configs[2] (B = 65536) 57.0 -> 58.8 M solves/s;
+    //   otherwise full on the caller's stream, swing then compacted on the split
+    //   stream -- B = 16384 45.5 vs 42.1 M, configs[1] 22.3 vs 18.5 M.
+    auto full_on = [&](hipStream_t st) {
+      if (variant == 3) hipLaunchKernelGGL((solve_kernel<3, N, real>), dim3((unsigned)a.B), dim3(NT), HMPC_DIAG_LDS_FULL, st, af);
 #ifdef HMPC_FULL2F_NV
-    else HMPC_FULL2F_LAUNCH(af, s);
+      else HMPC_FULL2F_LAUNCH(af, st);
 #else
-    else hipLaunchKernelGGL((solve_kernel<2, N, real>), dim3((unsigned)a.B), dim3(NT), 0, s, af);
+      else hipLaunchKernelGGL((solve_kernel<2, N, real>), dim3((unsigned)a.B), dim3(NT), 0, st, af);
 #endif
+    };
+    auto cmp_on = [&](hipStream_t st) { HMPC_CMP_LAUNCH(variant, ac, st); };
 #ifdef HMPC_SWING_LAUNCH
-    HMPC_SWING_LAUNCH(as, s2);
+    auto swing_on = [&](hipStream_t st) { HMPC_SWING_LAUNCH(as, st); };
 #else
-    (void)as;
+    auto swing_on = [&](hipStream_t) { (void)as; };
 #endif
-    HMPC_CMP_LAUNCH(variant, ac, s2);
+#ifndef HMPC_SWING_FIRST_B
+#define HMPC_SWING_FIRST_B 32768
+#endif
+    if (kSw && !a.lpt && a.B >= HMPC_SWING_FIRST_B) {
+      swing_on(s);
+      full_on(s);
+      cmp_on(s2);
+    } else {
+      full_on(s);
+      swing_on(s2);
+      cmp_on(s2);
+    }
     if (s2 != s) {
       if (hipEventRecord(a.split_join, s2) != hipSuccess) return false;
       if (hipStreamWaitEvent(s, a.split_join, 0) != hipSuccess) return false;

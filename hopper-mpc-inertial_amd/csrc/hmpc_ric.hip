@@ -1525,13 +1525,24 @@ __global__ void __launch_bounds__(kLptT) ric_buckets_kernel(SolveArgs a, int N, 
   const int64_t i = i0 + lane;
   const bool in = i < a.B;
   int nst = 0;
-#pragma unroll 8
-  for (int r = 0; r < 64; ++r) {
-    const int64_t ir = i0 + r;
-    const bool ok = ir < a.B && lane < N;
-    const double cv = a.C[(ok ? ir * a.C_bs + lane : 0)];
-    const int cnt = __builtin_popcountll(__ballot(ok && cv != 0.0));
-    nst = lane == r ? cnt : nst;
+  // 16 rows per batch: all 16 loads issued before the first ballot (one
+  // round trip per batch; a load-ballot pair per row serialised them)
+  const int64_t last = a.B - 1;
+  const int col = lane < N ? lane : 0;
+#pragma unroll 1
+  for (int r0 = 0; r0 < 64; r0 += 16) {
+    double cv[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int64_t ir = i0 + r0 + u;
+      cv[u] = a.C[(ir < last ? ir : last) * a.C_bs + col];
+    }
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const bool ok = i0 + r0 + u <= last && lane < N;
+      const int cnt = __builtin_popcountll(__ballot(ok && cv[u] != 0.0));
+      nst = lane == r0 + u ? cnt : nst;
+    }
   }
   const int k = in ? min(nst / W, nb - 1) : 0;
   uint64_t mine = 0;

@@ -80,6 +80,16 @@ __device__ __forceinline__ double msel(uint64_t m, double t, double f) {
 }
 // a 32-bit lane pattern in both halves
 constexpr uint64_t rep(uint32_t m) { return (uint64_t)m | ((uint64_t)m << 32); }
+// rep(M) materialised where it is used (a volatile s_mov): the sweeps' step
+// masks are loop-invariant inside the active set, and machine LICM hoisted
+// all of them out of it -- ~90 SGPR pairs live across the loop, 196 SGPR
+// spills into VGPR lanes and a readlane per reload
+template <uint32_t M>
+__device__ __forceinline__ uint64_t kmask() {
+  uint32_t v;
+  asm volatile("s_mov_b32 %0, %1" : "=s"(v) : "i"(M));
+  return ((uint64_t)v << 32) | v;
+}
 constexpr uint32_t lo_bits(int n) { return n >= 32 ? 0xffffffffu : ((1u << n) - 1u); }
 
 typedef __attribute__((address_space(3))) double lds_double;
@@ -260,7 +270,7 @@ constexpr int kRing = 4;
 // one load of the ring: lane mask (lanes that read M), byte offset from the
 // lane's base, which base (0: the forward base, 1: the backward base)
 struct Step {
-  uint64_t mask;
+  uint32_t mask;   // lanes of each half (replicated by kmask)
   int off;
 };
 
@@ -279,14 +289,14 @@ __device__ __forceinline__ double tri_fwd(double acc, unsigned fbase, unsigned z
   constexpr auto step = [](int j) constexpr -> Step {
     if (j < SA) {   // column s = j, lanes s < i < 16
       const int s = j;
-      return Step{rep(lo_bits(NA) & ~lo_bits(s + 1)), 8 * (L::cb(s) - s)};
+      return Step{lo_bits(NA) & ~lo_bits(s + 1), 8 * (L::cb(s) - s)};
     }
     if (j < SA + SX) {   // column t, lanes 16 <= i < NV
       const int t = j - SA;
-      return Step{rep(kLive & ~lo_bits(16)), 8 * (L::cb(t) - t)};
+      return Step{kLive & ~lo_bits(16), 8 * (L::cb(t) - t)};
     }
     const int s = 16 + (j - SA - SX);   // column s, lanes s < i < NV
-    return Step{rep(kLive & ~lo_bits(s + 1)), 8 * (L::cb(s) - s)};
+    return Step{kLive & ~lo_bits(s + 1), 8 * (L::cb(s) - s)};
   };
   auto addr = [&](auto jc) -> unsigned {
     constexpr int j = decltype(jc)::value;
@@ -294,7 +304,7 @@ __device__ __forceinline__ double tri_fwd(double acc, unsigned fbase, unsigned z
       return zaddr;
     } else {
       constexpr Step st = step(j);
-      return msel(st.mask, fbase + (unsigned)st.off, zaddr);
+      return msel(kmask<st.mask>(), fbase + (unsigned)st.off, zaddr);
     }
   };
   static_assert(NS >= kRing, "the ring is primed with real steps");
@@ -337,14 +347,14 @@ __device__ __forceinline__ double tri_bwd(double acc, unsigned bbase, unsigned z
   constexpr auto step = [](int j) constexpr -> Step {
     if (j < SB) {
       const int s = NV - 1 - j;
-      return Step{rep(lo_bits(s) & ~lo_bits(16)), 8 * s};
+      return Step{lo_bits(s) & ~lo_bits(16), 8 * s};
     }
     if (j < SB + SX) {
       const int s = NV - 1 - (j - SB);
-      return Step{rep(lo_bits(16)), 8 * s};
+      return Step{lo_bits(16), 8 * s};
     }
     const int s = NA - 1 - (j - SB - SX);
-    return Step{rep(lo_bits(s)), 8 * s};
+    return Step{lo_bits(s), 8 * s};
   };
   auto addr = [&](auto jc) -> unsigned {
     constexpr int j = decltype(jc)::value;
@@ -352,7 +362,7 @@ __device__ __forceinline__ double tri_bwd(double acc, unsigned bbase, unsigned z
       return zaddr;
     } else {
       constexpr Step st = step(j);
-      return msel(st.mask, bbase + (unsigned)st.off, zaddr);
+      return msel(kmask<st.mask>(), bbase + (unsigned)st.off, zaddr);
     }
   };
   static_assert(NS >= kRing, "the ring is primed with real steps");
@@ -378,6 +388,21 @@ __device__ __forceinline__ double tri_bwd(double acc, unsigned bbase, unsigned z
 
 constexpr int kPrioSwing = 1;
 
+// Diagnostic build only (-DHMPC_STAMPS, tools/phase_stamps.py): s_memtime at
+// the dense kernel's phase boundaries (slots 0..8; 1 == 2, the dynamics run
+// with the loads) and its accumulated active-set sub-phases (9..14), written
+// over each instance's x* row.  One wave runs both halves, so a pair shares
+// its stamps.
+#ifdef HMPC_STAMPS
+#define SW_STAMP(i) (stamp_[i] = __builtin_amdgcn_s_memtime())
+#define SW_TIC(v) const long long v = __builtin_amdgcn_s_memtime()
+#define SW_TOC(slot, v) (stamp_[slot] += __builtin_amdgcn_s_memtime() - (v))
+#else
+#define SW_STAMP(i) ((void)0)
+#define SW_TIC(v) ((void)0)
+#define SW_TOC(slot, v) ((void)0)
+#endif
+
 // ---------------------------------------------------------------------------
 // the kernel: block i solves instances 2i (lanes 0..31) and 2i + 1 (lanes
 // 32..63) of its class list
@@ -399,6 +424,10 @@ __global__ void __launch_bounds__(64, HMPC_SWING_WAVES) swing_kernel(SolveArgs a
   // instance (identical control flow) and stores nothing
   const int64_t b = a.list[valid ? i0 + h : i0];
   const double dt = a.dt;
+#ifdef HMPC_STAMPS
+  long long stamp_[16] = {0};
+#endif
+  SW_STAMP(0);
 
   // ---------------- phase 0: loads ------------------------------------------
   {
@@ -429,6 +458,7 @@ __global__ void __launch_bounds__(64, HMPC_SWING_WAVES) swing_kernel(SolveArgs a
       if (i < 12 * N) sm[L::XREF + i] = vr[it];
     });
     if (hl == 0) sm[L::ZR] = 0.0;
+    SW_STAMP(1);
     // ---------------- phase 1: gen_dt_dynamics, torque block (lane k < N)
     // (3f :71-94, 2f :70-94: B[9:12, 3:6] = J_w_inv Rz' dt, :86,89)
     if (hl < N) {
@@ -460,6 +490,7 @@ __global__ void __launch_bounds__(64, HMPC_SWING_WAVES) swing_kernel(SolveArgs a
     }
   }
   wsync();
+  SW_STAMP(2);
 
   // ---------------- phase 2: free response, cost-to-go, adjoint --------------
   // (lane r < 12 of a half holds component r; the cost-to-go's rotational
@@ -544,6 +575,7 @@ __global__ void __launch_bounds__(64, HMPC_SWING_WAVES) swing_kernel(SolveArgs a
     zrow = half_any(zbad1, h);
   }
   wsync();
+  SW_STAMP(3);
 
   // ---------------- phase 3: Hessian row (lower part) + gradient -------------
   // lane v < NV owns torque c = v % 3 of stage i = v / 3; lanes NV..31 are
@@ -600,6 +632,7 @@ __global__ void __launch_bounds__(64, HMPC_SWING_WAVES) swing_kernel(SolveArgs a
   }
   double wv = -hv;   // the forward sweep's accumulator (phase 4)
   wsync();           // union A (XREF / SS / AJ) is dead from here on
+  SW_STAMP(4);
   __builtin_amdgcn_s_setprio(kPrioSwing);
 
   // ---------------- phase 4: Cholesky ---------------------------------------
@@ -611,6 +644,9 @@ __global__ void __launch_bounds__(64, HMPC_SWING_WAVES) swing_kernel(SolveArgs a
   double dinv;
   {
     constexpr int CW = 4;
+    // depth of the column-chunk ring (3 one chunk further ahead; 2 for the
+    // 4-wave register budget)
+    constexpr int kCR = HMPC_SWING_WAVES >= 4 ? 2 : 3;
     constexpr int CBS = L::CBS;
     constexpr uint32_t kLive = lo_bits(NV);
     auto nldc = [](int ja, int ch) constexpr {   // b128 loads of chunk ch of [ja, NV)
@@ -663,13 +699,13 @@ __global__ void __launch_bounds__(64, HMPC_SWING_WAVES) swing_kernel(SolveArgs a
       }
       wv = fma(msel(m_gt, tk, 0.0), -hbc<k>(wv), wv);
       const unsigned cbase = colb[k & 1];
-      double2_ buf[3][CW / 2];
+      double2_ buf[kCR][CW / 2];
       auto load = [&](auto chc) __attribute__((always_inline)) {
         constexpr int ch = decltype(chc)::value;
         if constexpr (ch >= 1 && ch < NCH) {
           sfor<0, nldc(JA, ch)>([&](auto ic) __attribute__((always_inline)) {
             constexpr int i = decltype(ic)::value;
-            lds_ld2<8 * (JA + CW * ch + 2 * i)>(buf[ch % 3][i], cbase);
+            lds_ld2<8 * (JA + CW * ch + 2 * i)>(buf[ch % kCR][i], cbase);
           });
         }
       };
@@ -690,18 +726,23 @@ __global__ void __launch_bounds__(64, HMPC_SWING_WAVES) swing_kernel(SolveArgs a
           }
         });
       };
-      load(std::integral_constant<int, 1>{});
-      load(std::integral_constant<int, 2>{});
+      // chunks >= 1 through a kCR-deep ring: the prologue loads chunks
+      // 1 .. kCR-1, then ahead(k+1) issues its LDS ops, and iteration ch
+      // loads chunk ch + kCR - 1 before it waits for chunk ch
+      sfor<1, kCR>([&](auto chc) __attribute__((always_inline)) { load(chc); });
       if constexpr (NCH > 0) update(std::integral_constant<int, 0>{}, nb);
       if constexpr (k + 1 < NV) ahead(std::integral_constant<int, k + 1>{});
       sfor<1, NCH>([&](auto chc) __attribute__((always_inline)) {
         constexpr int ch = decltype(chc)::value;
-        load(std::integral_constant<int, ch + 2>{});
-        constexpr int younger = ch == 1 ? nl(JA, 2) + NAHEAD + nl(JA, 3)
-                              : ch == 2 ? NAHEAD + nl(JA, 3) + nl(JA, 4)
-                                        : nl(JA, ch + 1) + nl(JA, ch + 2);
-        lds_wait<younger>(buf[ch % 3][0], buf[ch % 3][1]);
-        update(chc, buf[ch % 3]);
+        load(std::integral_constant<int, ch + kCR - 1>{});
+        // LDS ops issued after chunk ch's loads
+        constexpr int younger = [&]() constexpr {
+          int y = ch <= kCR - 1 ? NAHEAD : 0;
+          for (int c = ch + 1; c <= ch + kCR - 1; ++c) y += nl(JA, c);
+          return y;
+        }();
+        lds_wait<younger>(buf[ch % kCR][0], buf[ch % kCR][1]);
+        update(chc, buf[ch % kCR]);
       });
       if constexpr (k + 1 < NV) lds_wait<0>(nb[0], nb[1]);
     });
@@ -714,12 +755,14 @@ __global__ void __launch_bounds__(64, HMPC_SWING_WAVES) swing_kernel(SolveArgs a
     dinv = active_lane ? sm[L::LC + L::cb(active_lane ? hl : 0)] : 1.0;   // 1 / L[v][v]
   }
 
+  SW_STAMP(5);
   const unsigned zaddr = lds_addr(sm + L::ZR);
   const unsigned fbase = lds_addr(sm + L::LC + hl);                                   // + 8 (cb(s) - s)
   const unsigned bbase = lds_addr(sm + L::LC + (active_lane ? L::cb(hl) - hl : 0));   // + 8 s
 
   // ---------------- phase 5: v0 = -L^-T L^-1 h --------------------------------
   double v = tri_bwd<L>(wv * dinv, bbase, zaddr, dinv);
+  SW_STAMP(6);
 #ifdef HMPC_SWING_DEBUG
   // (debug build, tools/swing_debug3.py: per lane v0, the first w and z, and
   // scalars of the first inner iteration, written over x*)
@@ -749,11 +792,13 @@ __global__ void __launch_bounds__(64, HMPC_SWING_WAVES) swing_kernel(SolveArgs a
   bool done = status != ST_SOLVED;
   while (!done) {
     // ---- slacks of my rows; the most violated over the half ----
+    SW_TIC(t_scan);
     double best = INFINITY;
     int bid = 0x7fffffff;
     if (active_lane && !(actmask & 1)) argmin_combine(best, bid, v + lim, 4 * hl);
     if (active_lane && !(actmask & 2)) argmin_combine(best, bid, lim - v, 4 * hl + 1);
     half_argmin(best, bid);
+    SW_TOC(9, t_scan);
     if (!(best < -kTol)) break;   // primal feasible: optimal
     const int p = bid;
     const int o = p >> 2;
@@ -762,8 +807,10 @@ __global__ void __launch_bounds__(64, HMPC_SWING_WAVES) swing_kernel(SolveArgs a
     const double np_me = hl == o ? sgn : 0.0;
     double u_plus = 0.0;
     // w = L^-1 n_p
+    SW_TIC(t_fwd);
     const double wfull = tri_fwd<L>(np_me, fbase, zaddr, dinv);
     const double wnorm2 = half_sum(wfull * wfull);
+    SW_TOC(10, t_fwd);
 #ifdef HMPC_SWING_DEBUG
     if (dbg_n == 0) {
       dbg1 = wfull;
@@ -777,6 +824,7 @@ __global__ void __launch_bounds__(64, HMPC_SWING_WAVES) swing_kernel(SolveArgs a
       const int qu = q;
       // w_perp = (I - Qw Qw') w and c = Qw' w (modified Gram-Schmidt, a
       // second pass when the first cancels more than half the norm)
+      SW_TIC(t_gs);
       double wp = wfull, zn = wnorm2;
       for (int pass = 0; pass < 2 && qu > 0; ++pass) {
         ladder<0, QM>(qu, [&](auto lc) __attribute__((always_inline)) {
@@ -791,8 +839,12 @@ __global__ void __launch_bounds__(64, HMPC_SWING_WAVES) swing_kernel(SolveArgs a
         if (enough) break;
       }
       wsync();
+      SW_TOC(11, t_gs);
       // primal direction z = L^-T w_perp
+      SW_TIC(t_bwd);
       const double zi = tri_bwd<L>(wp, bbase, zaddr, dinv);
+      SW_TOC(12, t_bwd);
+      SW_TIC(t_dual);
       // dual direction r = R^-1 c (lanes l < q), back substitution
       double rcur = hl < qu ? cbv[hl < qu ? hl : 0] : 0.0, rmine = 0.0;
       for (int l = qu - 1; l >= 0; --l) {
@@ -828,6 +880,8 @@ __global__ void __launch_bounds__(64, HMPC_SWING_WAVES) swing_kernel(SolveArgs a
       if (hl < qu) ua[hl] -= t * rmine;
       u_plus += t;
       wsync();
+      SW_TOC(13, t_dual);
+      SW_TIC(t_upd);
       if (has_z && t == t2) {
         // ---- add p: new basis column w_perp / |w_perp|, R column [c; rho] ----
         if (qu >= QM) { status = a.ovf_count ? ST_OVERFLOW : ST_NUMERICAL; done = true; break; }
@@ -841,6 +895,7 @@ __global__ void __launch_bounds__(64, HMPC_SWING_WAVES) swing_kernel(SolveArgs a
         if (hl == o) actmask |= 1 << (p & 3);
         q = qu + 1;
         wsync();
+        SW_TOC(14, t_upd);
         break;
       }
       // ---- drop active constraint kdrop ----
@@ -891,10 +946,12 @@ __global__ void __launch_bounds__(64, HMPC_SWING_WAVES) swing_kernel(SolveArgs a
         for (int l = 0; l < QM; ++l) Qw[l] = (l == qu - 1) ? 0.0 : Qw[l];
         q = qu - 1;
         wsync();
+        SW_TOC(14, t_upd);
       }
     }
   }
   __builtin_amdgcn_s_setprio(0);
+  SW_STAMP(7);
 
   // an overflowed instance writes nothing but its status and its place in
   // the overflow list (x_lin may be this solve's input, mpcontrol shift)
@@ -961,6 +1018,11 @@ __global__ void __launch_bounds__(64, HMPC_SWING_WAVES) swing_kernel(SolveArgs a
     xo[32 + hl] = dbg1;
     xo[64 + hl] = dbg2;
     xo[96 + hl] = dbg3;
+    wsync();
+#endif
+#ifdef HMPC_STAMPS
+    SW_STAMP(8);
+    if (hl < 16) xo[hl] = __longlong_as_double(stamp_[hl]);   // (lane-uniform stamps)
     wsync();
 #endif
     if (valid) {
