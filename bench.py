@@ -241,7 +241,6 @@ def main():
     if args.precision == 'f32_refined':
         ctx.set_refinement(args.refine)
     ctx.set_order(args.order)
-    kernel = ctx.kernel_name
     out = dict(u=torch.empty((B, N, 6), dtype=torch.float64, device=dev),
                x=torch.empty((B, N + 1, 12), dtype=torch.float64, device=dev),
                obj=torch.empty(B, dtype=torch.float64, device=dev),
@@ -275,6 +274,8 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
+    kernel = ctx.kernel_name   # (the classes this batch's solves ran)
+    ovf0 = ctx.overflow_total   # instances the overflow pass re-solved so far
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
            for _ in range(args.steps)]
     if world > 1:
@@ -295,6 +296,7 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
     el, kern_ms_max = float(tt[0]), float(tt[1])
 
+    ovf_step = (ctx.overflow_total - ovf0) / args.steps
     st = last[0]['status'].cpu().numpy()
     it = out['iters'].cpu().numpy()
     act = out['active'].cpu().numpy()
@@ -400,6 +402,10 @@ def main():
             'solved_frac_min_rank': float(sf[0]),
             'iters_mean': iters_mean, 'iters_max': int(it.max()),
             'active_mean': q_mean, 'active_max': int(act.max()),
+            # the slow fp64 pass (hmpc_overflow_total): active sets beyond the
+            # main pass's capacity; for f32_refined also the fp64-check and
+            # convergence fallbacks
+            'overflow_pass': {'instances_per_step': ovf_step, 'frac': ovf_step / B},
             'parity_sample': parity,
             'dist': dist_info,
         }

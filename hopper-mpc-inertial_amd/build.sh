@@ -70,10 +70,17 @@ for n in $F32_HORIZONS; do
     pids+=($!)
     CMPOBJS="$CMPOBJS $BDIR/hmpc_kernels_n${n}_f32_cmp.o"
   fi
-  # fp32 + fp64 refinement (HMPC_PREC_F32_REFINED)
+  # fp32 + fp64 refinement (HMPC_PREC_F32_REFINED), split like the others:
+  # every class at 2 waves / SIMD (no scratch spill)
   $HIPCC $FLAGS -DHMPC_INST_N=$n -DHMPC_REAL=float -DHMPC_F32_REFINE=1 -DHMPC_LAUNCH_SUFFIX=_f32r \
-    "-DHMPC_WAVES_PER_EU(W)=$F32_WAVES" -c csrc/hmpc_kernels.hip -o $BDIR/hmpc_kernels_n${n}_f32r.o "$@" &
+    "-DHMPC_WAVES_PER_EU(W)=2" $F32C -c csrc/hmpc_kernels.hip -o $BDIR/hmpc_kernels_n${n}_f32r.o "$@" &
   pids+=($!)
+  if [ -n "$F32C" ]; then
+    $HIPCC $FLAGS -DHMPC_INST_N=$n -DHMPC_REAL=float -DHMPC_F32_REFINE=1 -DHMPC_LAUNCH_SUFFIX=_f32r \
+      "-DHMPC_WAVES_PER_EU(W)=2" $F32C -DHMPC_CMP_ONLY -c csrc/hmpc_kernels.hip -o $BDIR/hmpc_kernels_n${n}_f32r_cmp.o "$@" &
+    pids+=($!)
+    CMPOBJS="$CMPOBJS $BDIR/hmpc_kernels_n${n}_f32r_cmp.o"
+  fi
 done
 $HIPCC $FLAGS "-DHMPC_HORIZON_LIST(X)=$LIST" "-DHMPC_F32_LIST(X)=$F32LIST" "-DHMPC_F32R_LIST(X)=$F32LIST" -c csrc/hmpc_dispatch.cpp -o $BDIR/hmpc_dispatch.o &
 pids+=($!)

@@ -41,6 +41,7 @@ struct hmpc_ctx {
   // buckets) | list of ovf_cap ids] and the global R blocks of its workgroups
   int32_t* ovf = nullptr;
   int64_t ovf_cap = 0;
+  unsigned long long* ovf_total = nullptr;   // hmpc_overflow_total
   // the counters need a zeroing before the next solve (fresh buffer, or a
   // solve whose overflow pass -- which zeroes them at its end -- did not run)
   bool ovf_dirty = true;
@@ -54,6 +55,9 @@ struct hmpc_ctx {
   // the last Riccati solve at a one-wave horizon ran the fused kernel (no
   // per-instance K / Dinv buffer: beyond its 4 GB bound or out of memory)
   bool ric_fused = false;
+  // the last dense solve ran in longest-first order (the all-swing class
+  // then stays in the compacted class, hmpc_kernels.hip)
+  bool dense_lpt = false;
   hipStream_t split_stream = nullptr;   // the compacted class's stream
   hipEvent_t split_fork = nullptr, split_join = nullptr;
   // Riccati kernel: per-workgroup K / Dinv workspace of its resident grid
@@ -106,6 +110,7 @@ hmpc::SolveArgs make_args(hmpc_ctx* c, int64_t B, const double* x_in, const doub
   a.C_bs = N;
   a.ws = nullptr; a.ws_stride = 0; a.ws_groups = 0;
   a.ovf_count = nullptr; a.ovf_list = nullptr; a.rws = nullptr; a.rws_stride = 0;
+  a.ovf_total = nullptr;
   a.work = nullptr; a.kws = nullptr; a.kws_stride = 0; a.ric_groups = 0;
   a.kinst = nullptr; a.kinst_stride = 0;
   a.split_count = nullptr; a.split_list = nullptr; a.list = nullptr; a.list_count = nullptr;
@@ -236,11 +241,21 @@ int prepare_ric(hmpc_ctx* c, int64_t B, hmpc::SolveArgs& a) {
   a.ovf_count = c->ovf;
   a.work = c->ovf + 1;
   a.ovf_list = c->ovf + kOvfHeader;
+  if (!c->ovf_total) {
+    if (hipMalloc(&c->ovf_total, sizeof(unsigned long long)) != hipSuccess ||
+        hipMemset(c->ovf_total, 0, sizeof(unsigned long long)) != hipSuccess) {
+      c->ovf_total = nullptr;
+      c->err = "overflow total hipMalloc";
+      return HMPC_ERR_NOMEM;
+    }
+  }
+  a.ovf_total = c->ovf_total;
   // the dense kernel's split launch (compacted kernel for the instances with
   // few free variables): class counts next to the overflow counters, which
   // the overflow pass zeroes together at its end
   const bool split = (k == hmpc::Kernel::Dense && hmpc::dense_split_nv(c->N, 0) > 0) ||
-                     (k == hmpc::Kernel::DenseF32 && hmpc::dense_split_nv(c->N, 1) > 0);
+                     (k == hmpc::Kernel::DenseF32 && hmpc::dense_split_nv(c->N, 1) > 0) ||
+                     (k == hmpc::Kernel::DenseF32R && hmpc::dense_split_nv(c->N, 2) > 0);
   if (split && c->N + 1 <= kOvfHeader - 3) {
     // (up to N + 1 stance-count buckets of B entries -- longest-first order --
     // or the three class lists)
@@ -258,6 +273,7 @@ int prepare_ric(hmpc_ctx* c, int64_t B, hmpc::SolveArgs& a) {
     a.split_list = c->split;
     a.split_nbkt = c->N + 1;
     a.lpt = longest_first(c, B) ? 1 : 0;
+    c->dense_lpt = a.lpt != 0;
     a.split_stream = c->split_stream;
     a.split_fork = c->split_fork;
     a.split_join = c->split_join;
@@ -401,7 +417,7 @@ int check_solve_args(hmpc_ctx* c, int64_t B, const void* x_in, const void* x_lin
 
 extern "C" {
 
-int hmpc_version(void) { return 10400; }
+int hmpc_version(void) { return 10500; }
 
 int hmpc_supported_horizons(int variant, int* Ns, int cap) {
   return hmpc::supported_horizons(variant, Ns, cap);
@@ -437,6 +453,7 @@ int hmpc_destroy(hmpc_ctx* c) {
   if (c->ovf) (void)hipFree(c->ovf);
   if (c->rws) (void)hipFree(c->rws);
   if (c->split) (void)hipFree(c->split);
+  if (c->ovf_total) (void)hipFree(c->ovf_total);
   if (c->split_stream) (void)hipStreamDestroy(c->split_stream);
   if (c->split_fork) (void)hipEventDestroy(c->split_fork);
   if (c->split_join) (void)hipEventDestroy(c->split_join);
@@ -450,6 +467,17 @@ int hmpc_destroy(hmpc_ctx* c) {
 }
 
 const char* hmpc_last_error(hmpc_ctx* c) { return c ? c->err.c_str() : ""; }
+
+int hmpc_overflow_total(hmpc_ctx* c, int64_t* total) {
+  if (!c || !total) return HMPC_ERR_ARG;
+  *total = 0;
+  if (!c->ovf_total) return HMPC_OK;   // no solve with an overflow pass yet
+  if (c->has_last) HMPC_HIP(c, hipEventSynchronize(c->last_ev));
+  unsigned long long v = 0;
+  HMPC_HIP(c, hipMemcpy(&v, c->ovf_total, sizeof v, hipMemcpyDeviceToHost));
+  *total = (int64_t)v;
+  return HMPC_OK;
+}
 
 int hmpc_active_capacity(hmpc_ctx* c) {
   if (!c) return -1;
@@ -475,8 +503,14 @@ const char* hmpc_kernel_name(hmpc_ctx* c) {
   if (!c) return "";
   const bool v3 = c->variant == HMPC_VARIANT_3F;
   switch (hmpc::pick_kernel(c->variant, c->N, c->precision)) {
-    case hmpc::Kernel::Dense:
-      return hmpc::dense_name(c->variant, c->N, 0);
+    case hmpc::Kernel::Dense: {
+      // (the classes of the last solve: in longest-first order the all-swing
+      // windows stay in the compacted class)
+      const char* n = hmpc::dense_name(c->variant, c->N, 0);
+      const char* rest = strstr(n, " + ");
+      if (c->dense_lpt && strncmp(n, "hmpc::swing_kernel", 18) == 0 && rest) return rest + 3;
+      return n;
+    }
     case hmpc::Kernel::DenseF32:
       return hmpc::dense_name(c->variant, c->N, 1);
     case hmpc::Kernel::DenseF32R:

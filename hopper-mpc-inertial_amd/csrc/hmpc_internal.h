@@ -55,6 +55,9 @@ struct SolveArgs {
   // per resident workgroup).  ovf_count == nullptr: overflow = ST_NUMERICAL.
   int32_t* ovf_count;
   int32_t* ovf_list;
+  // running total of the instances the overflow pass re-solved on this
+  // context (hmpc_overflow_total), or nullptr
+  unsigned long long* ovf_total;
   double* rws;
   int64_t rws_stride;
   // Riccati kernel (persistent): instance counter (zeroed before the launch),

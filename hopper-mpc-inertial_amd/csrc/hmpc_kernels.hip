@@ -565,8 +565,11 @@ constexpr int kPrioFullBase = 2;
 // waves / SIMD of the split's compacted class (NVM <= kCmp3W): fp64 3
 // (<= 168 VGPRs), fp32 4 (<= 128, 12 B/lane of spill); a wider compacted
 // kernel (2f's 5N-wide full class) runs like the full one, fp64 2, fp32 3
-constexpr int kCmpWaves = sizeof(real) == 4 ? 4 : 3;
-constexpr int kWideCmpWaves = sizeof(real) == 4 ? 3 : 2;
+// (the fp32 + fp64 refinement build: 2 waves / SIMD for every class, the refinement's
+// fp64 state fits without scratch: full 214 VGPRs; at 3 waves the compacted
+// class spilled 60 B/lane)
+constexpr int kCmpWaves = kRefine ? 2 : (sizeof(real) == 4 ? 4 : 3);
+constexpr int kWideCmpWaves = kRefine ? 2 : (sizeof(real) == 4 ? 3 : 2);
 constexpr int kCmp3W = 48;
 // The kernel's argument block through an opaque kernarg-segment pointer:
 // reads through it are fresh scalar loads where they stand, so the compiler
@@ -2101,7 +2104,11 @@ bool HMPC_CAT(HMPC_CAT(launch_solve_n, HMPC_INST_N), HMPC_LAUNCH_SUFFIX)(int var
       const int smax = (HMPC_CMP_NV - 3 * N) / (variant == 3 ? 3 : 2);
       ac.list = af.list = a.split_list;
       ac.list_count = af.list_count = a.split_count;
-      ac.lpt_lo = kSw ? 1 : 0;
+      // (the all-swing class runs in index order only: with longest-first
+      // order at B = 4096 it cost 8-12 %, configs[1] 24.3 -> 22.3 M, since
+      // those windows are the cheapest and fill the tail as bucket 0 of the
+      // compacted class; profiles/r05_ab.json)
+      ac.lpt_lo = 0;
       ac.lpt_hi = smax;
       af.lpt_lo = smax + 1;
       af.lpt_hi = N;
@@ -2150,7 +2157,7 @@ bool HMPC_CAT(HMPC_CAT(launch_solve_n, HMPC_INST_N), HMPC_LAUNCH_SUFFIX)(int var
       cmp_on(s2);
     } else {
       full_on(s);
-      swing_on(s2);
+      if (!a.lpt) swing_on(s2);
       cmp_on(s2);
     }
     if (s2 != s) {

@@ -1495,6 +1495,7 @@ __global__ void __launch_bounds__(RT) ric_overflow_kernel(SolveArgs a, int N) {
   if (threadIdx.x == 0) {
     __threadfence();
     if (atomicAdd(a.ovf_count + 2, 1) == (int)gridDim.x - 1) {
+      if (a.ovf_total) atomicAdd(a.ovf_total, (unsigned long long)n);
       atomicExch(a.ovf_count, 0);
       atomicExch(a.ovf_count + 1, 0);
       atomicExch(a.ovf_count + 2, 0);

@@ -60,6 +60,7 @@ SIGNATURES = {
     'hmpc_last_error': (ctypes.c_char_p, [_VP]),
     'hmpc_kernel_name': (ctypes.c_char_p, [_VP]),
     'hmpc_active_capacity': (ctypes.c_int, [_VP]),
+    'hmpc_overflow_total': (ctypes.c_int, [_VP, _VP]),
     'hmpc_time_solve_batch': (ctypes.c_int, [_VP, ctypes.c_int64] + [_VP] * 11
                               + [ctypes.c_int, _VP, ctypes.POINTER(ctypes.c_double)]),
 }
@@ -179,6 +180,14 @@ class Context:
     def active_capacity(self):
         """Active-set capacity of the main pass (hmpc_active_capacity)."""
         return int(self._lib.hmpc_active_capacity(self._h))
+
+    @property
+    def overflow_total(self):
+        """Instances the overflow pass re-solved on this context so far
+        (hmpc_overflow_total; waits for the last solve)."""
+        v = ctypes.c_int64(0)
+        self._check(self._lib.hmpc_overflow_total(self._h, ctypes.byref(v)), 'hmpc_overflow_total')
+        return int(v.value)
 
     def close(self):
         if getattr(self, '_h', None):

@@ -98,7 +98,8 @@ typedef struct hmpc_ctx hmpc_ctx;
    build, HMPC_PREC_F64_RICCATI / _F64_DENSE / _F32_GENERIC, hmpc_kernel_name,
    hmpc_active_capacity, hmpc_plan_batch, hmpc_gait_batch, HMPC_VARIANT_CAS;
    1.3.0 = + hmpc_solve_batch_stats, HMPC_PREC_F32_REFINED, hmpc_set_refinement;
-   1.4.0 = + hmpc_set_order */
+   1.4.0 = + hmpc_set_order;
+   1.5.0 = + hmpc_overflow_total */
 int hmpc_version(void);
 
 /* Which horizons have a dedicated (one- or two-wavefront) kernel for
@@ -273,6 +274,13 @@ const char* hmpc_kernel_name(hmpc_ctx* ctx);
    (capacity 6N) inside the same call, so this is a performance figure, not a
    limit (0 for the generic kernel, which has no overflow pass). */
 int hmpc_active_capacity(hmpc_ctx* ctx);
+
+/* Instances the overflow pass has re-solved on this context since it was
+   created: the active sets that outgrew the main pass's capacity, and (the
+   fp32 + fp64 refinement build) the instances whose fp64 check or
+   convergence test failed.  Waits for the context's last solve.  No
+   reference analogue: it reports where the GPU path spends its slow pass. */
+int hmpc_overflow_total(hmpc_ctx* ctx, int64_t* total);
 
 /* Last HIP error string of this context ("" if none). */
 const char* hmpc_last_error(hmpc_ctx* ctx);

@@ -57,10 +57,14 @@ int main() {
          HMPC_ERR_ARG);
   EXPECT(hmpc_last_error(nullptr)[0] == '\0');
   EXPECT(hmpc_kernel_name(nullptr)[0] == '\0');
+  int64_t ot = -1;
+  EXPECT(hmpc_overflow_total(nullptr, &ot) == HMPC_ERR_ARG);
   if (rc == HMPC_OK && c) {   // (a GPU host) the argument checks of a live context
     EXPECT(hmpc_solve_batch(c, -1, d, d, d, d, d, nullptr, d, d, d, s, s, nullptr) == HMPC_ERR_ARG);
     EXPECT(hmpc_solve_batch(c, 1, nullptr, d, d, d, d, nullptr, d, d, d, s, s, nullptr) == HMPC_ERR_ARG);
     EXPECT(hmpc_set_precision(c, 99) == HMPC_ERR_ARG);
+    EXPECT(hmpc_overflow_total(c, nullptr) == HMPC_ERR_ARG);
+    EXPECT(hmpc_overflow_total(c, &ot) == HMPC_OK && ot == 0);
     EXPECT(hmpc_time_solve_batch(c, 1, d, d, d, d, d, nullptr, d, d, d, s, s, 0, nullptr, &ms) == HMPC_ERR_ARG);
     EXPECT(hmpc_destroy(c) == HMPC_OK);
   }

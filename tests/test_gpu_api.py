@@ -72,7 +72,8 @@ def test_kernel_names(hm):
     assert make(hm, 10, 'f64_generic').kernel_name == 'hmpc::wide_kernel<3, double>'
     assert make(hm, 10, 'f32').kernel_name == ('hmpc::solve_kernel<3, 10, float, 48, 13> + '
                                                'hmpc::solve_kernel<3, 10, float, 0, 0>')   # fp32 split
-    assert make(hm, 10, 'f32_refined').kernel_name == 'hmpc::solve_kernel<3, 10, float, 0, 0>'
+    assert make(hm, 10, 'f32_refined').kernel_name == ('hmpc::solve_kernel<3, 10, float, 48, 13> + '
+                                                       'hmpc::solve_kernel<3, 10, float, 0, 0>')   # split (round 5)
     assert make(hm, 20, 'f32').kernel_name == 'hmpc::wide_kernel<3, float>'   # no fp32 dense build
     assert make(hm, 10, 'f32_generic').kernel_name == 'hmpc::wide_kernel<3, float>'
 

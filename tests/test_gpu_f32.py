@@ -111,7 +111,9 @@ def test_fp32_refined_meets_the_fp64_tolerance(hm, variant, curve, musweep):
     inst = hmpc_plan.sample_instances(B, N, curve=curve, seed=93,
                                       mu_sweep=(0.3, 1.2) if musweep else None)
     g, name = solve(hm, 'f32_refined', inst, N, variant, refine=5)
-    assert name == f'hmpc::solve_kernel<{variant[0]}, 10, float, 0, 0>'
+    v = variant[0]
+    full = f'hmpc::solve_kernel<{v}, 10, float, 0, 0>' if v == '3' else 'hmpc::solve_kernel<2, 10, float, 50, 20>'
+    assert name == f'hmpc::solve_kernel<{v}, 10, float, 48, 13> + {full}', name   # split (round 5)
     ref = port.solve_batch(variant, N, inst['x_in'], inst['x_lin'], inst['x_ref'], inst['pf'], inst['C'],
                            mu=inst['mu'], nthreads=16)
     assert np.array_equal(g['status'], ref['status'])
@@ -148,9 +150,20 @@ def test_fp32_refined_unconverged_goes_to_fp64(hm):
     from oracle import port
     N, B = 10, 256
     inst = hmpc_plan.sample_instances(B, N, curve=True, seed=95)
-    g, _ = solve(hm, 'f32_refined', inst, N, '3f', refine=1)
+    c = hmpc_plan.runner_constants()
+    cx = hm.Context('3f', N, t=c['t'], m=c['m'], g=c['g'], mu=1.0, Jinv=c['Jinv'], rh=c['rh'],
+                    precision='f32_refined')
+    cx.set_refinement(1)
+    g = cx.solve_host(inst['x_in'], inst['x_lin'], inst['x_ref'], inst['pf'], inst['C'], mu=inst['mu'])
+    fallbacks = cx.overflow_total   # (hmpc_overflow_total)
+    cx.set_refinement(5)
+    cx.solve_host(inst['x_in'], inst['x_lin'], inst['x_ref'], inst['pf'], inst['C'], mu=inst['mu'])
+    fallbacks5 = cx.overflow_total - fallbacks
+    cx.close()
     ref = port.solve_batch('3f', N, inst['x_in'], inst['x_lin'], inst['x_ref'], inst['pf'], inst['C'],
                            mu=inst['mu'], nthreads=16)
     assert np.array_equal(g['status'], ref['status'])
     ok = ref['status'] == 0
     assert np.abs(g['u'][ok] - ref['u'][ok]).max() <= 1e-6
+    assert fallbacks >= ok.sum()          # every solved instance went to the fp64 pass
+    assert fallbacks5 < 0.05 * B, fallbacks5   # five corrections converge almost everywhere

@@ -1,8 +1,10 @@
 """Instance order (hmpc_set_order): the dense split's class lists and the
 Riccati kernel's work queue served longest-first (stance-stage buckets, most
 stance stages first) or in batch index order.  Each instance is solved by the
-same kernel either way, so the results must be bit-identical between the
-orders, and equal to the C port's; the overflow pass and the self-resetting
+same kernel either way -- except the dense N = 10 all-swing windows, which the
+swing class (hmpc_swing.hip) solves in index order and the compacted class in
+the longest-first queue -- so the results must be bit-identical between the
+orders (those windows: within 1e-9), and equal to the C port's; the overflow pass and the self-resetting
 bucket counters must survive alternating orders on one context."""
 import numpy as np
 import pytest
@@ -24,6 +26,23 @@ def context(hm, variant, N):
     import hmpc_plan
     c = hmpc_plan.runner_constants()
     return hm.Context(variant, N, t=c['t'], m=c['m'], g=c['g'], mu=1.0, Jinv=c['Jinv'], rh=c['rh'])
+
+
+def same_across_orders(a, b, C, N):
+    """a (longest-first) and b (index order) bit-identical, except the dense
+    N = 10 all-swing windows (another kernel under 'index': the swing class),
+    which agree within 1e-9 with equal statuses."""
+    B = len(a['status'])
+    sw = np.zeros(B, bool)
+    if N == 10:
+        sw = ~(np.asarray(C).reshape(B, -1)[:, :N] != 0).any(axis=1)
+    for k in a:
+        assert np.array_equal(a[k][~sw], b[k][~sw]), k
+    assert np.array_equal(a['status'][sw], b['status'][sw])
+    ok = sw & (b['status'] == 0)
+    for k in ('u', 'x'):
+        assert np.abs(a[k][ok] - b[k][ok]).max(initial=0.0) <= 1e-9, k
+    assert (np.abs(a['obj'][ok] - b['obj'][ok]) <= 1e-12 * np.abs(b['obj'][ok])).all()
 
 
 @pytest.mark.parametrize('variant,N,B,curve,musweep', [
@@ -50,8 +69,7 @@ def test_orders_agree_bit_for_bit(hm, variant, N, B, curve, musweep):
         res.setdefault(order, r)
     cx.close()
     a, b = res['longest_first'], res['index']
-    for k in a:
-        assert np.array_equal(a[k], b[k]), k
+    same_across_orders(a, b, inst['C'], N)
     n = min(B, 256)
     ref = port.solve_batch(variant, N, *(v[:n] for v in args), mu=inst['mu'][:n], nthreads=16)
     assert np.array_equal(a['status'][:n], ref['status'])
@@ -77,8 +95,7 @@ def test_longest_first_with_overflow(hm):
     cx.set_order('index')
     b = cx.solve_host(*args, mu=inst['mu'])
     cx.close()
-    for k in a:
-        assert np.array_equal(a[k], b[k]), k
+    same_across_orders(a, b, inst['C'], N)
     ref = port.solve_batch('3f', N, *args, mu=inst['mu'], nthreads=16)
     assert np.array_equal(a['status'], ref['status'])
     ok = ref['status'] == 0

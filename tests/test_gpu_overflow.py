@@ -16,7 +16,7 @@ import os
 
 import numpy as np
 import pytest
-from conftest import DENSE10_3F
+from conftest import DENSE10_3F_LPT
 
 torch = pytest.importorskip('torch')
 
@@ -81,7 +81,7 @@ def solve_both(hm, N, inst, precision):
     return gpu, ref, kernel, cap
 
 
-@pytest.mark.parametrize('precision,kernel', [('f64', DENSE10_3F),
+@pytest.mark.parametrize('precision,kernel', [('f64', DENSE10_3F_LPT),   # (B = 48: longest-first)
                                              ('f64_riccati', 'hmpc::ric_kernel<3, 2, 0, 0, 0>')])
 def test_overflow_n10(hm, precision, kernel):
     N, B = 10, 48

@@ -221,3 +221,31 @@ def test_device_mpcontrol_matches_dropin(hm):
         assert out['status'].item() == 0
         assert np.array_equal(out['u'][0].cpu().numpy(), U)
         assert np.array_equal(xprev[0].cpu().numpy(), mpc.x.value)
+
+
+@pytest.mark.parametrize('variant,curve', [('3f', False), ('2f', False), ('3f', True)])
+def test_dense_n20_forced(hm, variant, curve):
+    """The two-wave dense kernel at N = 20 (HMPC_PREC_F64_DENSE, an A/B-only
+    precision; the default N = 20 path is the Riccati kernel): statuses, u*,
+    x* and the objective against the C port.  tools/exec_lint.py reports
+    exec-masked spill copies in this kernel (tests/test_exec_lint.py): this
+    checks their values are not read by lanes outside their regions."""
+    import hmpc_plan
+    from oracle import hmpc_oracle as ho
+    from oracle import port
+    N, B = 20, 256
+    inst = hmpc_plan.sample_instances(B, N, curve=curve, seed=77, mu_sweep=(0.3, 1.2))
+    c = ho.runner_constants()
+    cx = hm.Context(variant, N, t=c['t'], m=c['m'], g=c['g'], mu=1.0, Jinv=c['Jinv'], rh=c['rh'],
+                    precision='f64_dense')
+    assert cx.kernel_name == f'hmpc::solve_kernel<{variant[0]}, 20, double, 0, 0>'
+    g = cx.solve_host(inst['x_in'], inst['x_lin'], inst['x_ref'], inst['pf'], inst['C'], mu=inst['mu'])
+    cx.close()
+    ref = port.solve_batch(variant, N, inst['x_in'], inst['x_lin'], inst['x_ref'], inst['pf'], inst['C'],
+                           mu=inst['mu'], nthreads=16)
+    assert np.array_equal(g['status'], ref['status'])
+    ok = ref['status'] == 0
+    assert ok.mean() > 0.9
+    assert np.abs(g['u'][ok] - ref['u'][ok]).max() <= U_TOL
+    assert np.abs(g['x'][ok] - ref['x'][ok]).max() <= U_TOL
+    assert (np.abs(g['obj'][ok] - ref['obj'][ok]) / np.abs(ref['obj'][ok])).max() <= OBJ_RTOL
