@@ -77,6 +77,9 @@ constexpr bool kRefine = kF32 && HMPC_F32_REFINE;
 constexpr double kRefineTol = 1e-9;
 // and the largest last correction accepted as converged
 constexpr double kRefineDu = 4e-6;
+// ... and the early exit of the corrections (HMPC_REFINE_NO_EARLY_EXIT: always
+// a.refine of them)
+constexpr double kRefineStop = 4e-7;
 // feasibility tolerance of the slack scan and the relative threshold on
 // |w_perp|^2 for a usable primal direction, per precision
 constexpr real kTolR = kF32 ? real(2e-4) : real(kTol);
@@ -1597,6 +1600,9 @@ solve_kernel(SolveArgs a) {
     static_assert(W == 1, "the refinement runs in one-wave kernels");
     if (uni(status) != ST_SOLVED && a.ovf_count) status = ST_OVERFLOW;
     if (uni(status) == ST_SOLVED) {
+      // stamps (diagnostic build): 7 = the refinement's start, 15 = cycles in
+      // the corrections, 8 = the end of the fp64 check
+      HMPC_STAMP(7);
       const SolveArgs& ka = opaque_args(a);   // (fresh loads of the arguments)
       double* d64 = reinterpret_cast<double*>(sm + L::R64);
       double* dlo = reinterpret_cast<double*>(sm + L::R64LO);
@@ -1713,6 +1719,7 @@ solve_kernel(SolveArgs a) {
       double objl = 0.0;
       const int nref = ka.refine;
       double lastdu = INFINITY;   // |du| of the last correction (no correction: not converged)
+      HMPC_TIC(t_ref);
 #pragma unroll 1
       for (int it = 0; it < nref; ++it) {
         rollout(std::false_type{}, nullptr, objl);
@@ -1781,7 +1788,13 @@ solve_kernel(SolveArgs a) {
         lam += dlam;
         if (active_lane) dlo[L::DU + fidx] = u64;
         B::sync();
+#ifndef HMPC_REFINE_NO_EARLY_EXIT
+        // converged: a correction below kRefineStop on every lane leaves an
+        // error <= 0.25 x kRefineStop = 1e-7 (contraction <= cond x eps32 <= 0.2)
+        if (!__ballot(lastdu > kRefineStop)) break;
+#endif
       }
+      HMPC_TOC(15, t_ref);
       // outputs: x* (staged over L, dead now) and the objective from an fp64
       // rollout of the refined u
       double* xo = reinterpret_cast<double*>(sm + ((L::XO + 1) & ~1));
@@ -1809,8 +1822,15 @@ solve_kernel(SolveArgs a) {
       } else {
         B::sync();
         if (tid < L::NVF) ka.u[b * L::NVF + tid] = dlo[L::DU + tid];
+#ifndef HMPC_STAMPS
         if (ka.x)
           for (int i = tid; i < 12 * (N + 1); i += NT) ka.x[b * 12 * (N + 1) + i] = xo[i];
+#else
+        HMPC_STAMP(8);
+        if (ka.x && tid == 0)
+          for (int i = 0; i < 16; ++i)
+            reinterpret_cast<long long*>(ka.x)[b * 12 * (N + 1) + i] = stamp_[i];
+#endif
         if (tid == 0) {
           if (ka.obj) ka.obj[b] = objv;
           ka.status[b] = ST_SOLVED;
