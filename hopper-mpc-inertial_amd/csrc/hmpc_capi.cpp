@@ -170,9 +170,24 @@ constexpr int64_t kRicLptPerGroup = 8;
 bool longest_first(const hmpc_ctx* c, int64_t B) {
   if (c->order == HMPC_ORDER_INDEX) return false;
   if (c->order == HMPC_ORDER_LONGEST_FIRST) return true;
-  if (hmpc::pick_kernel(c->variant, c->N, c->precision) == hmpc::Kernel::Riccati)
-    return B <= kRicLptPerGroup * (int64_t)c->ric_groups;
+  if (hmpc::pick_kernel(c->variant, c->N, c->precision) == hmpc::Kernel::Riccati)   // (at most one
+    // instance per resident workgroup: all start at once, the order is moot and
+    // the bucket pass would be pure latency -- the Runner's B = 1)
+    return B > (int64_t)c->ric_groups && B <= kRicLptPerGroup * (int64_t)c->ric_groups;
   return B <= kDenseLptMaxB;
+}
+
+// The context's second stream and its fork / join events (the dense split's
+// concurrent class).
+int ensure_fork(hmpc_ctx* c) {
+  if (c->split_stream) return HMPC_OK;
+  if (hipStreamCreateWithFlags(&c->split_stream, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&c->split_fork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->split_join, hipEventDisableTiming) != hipSuccess) {
+    c->err = "split stream / events";
+    return HMPC_ERR_HIP;
+  }
+  return HMPC_OK;
 }
 
 // The class / bucket lists: nlist lists of B entries (grow-only).
@@ -261,14 +276,8 @@ int prepare_ric(hmpc_ctx* c, int64_t B, hmpc::SolveArgs& a) {
     // or the three class lists)
     int rc = ensure_split(c, B, c->N + 1 > 3 ? c->N + 1 : 3, "split list hipMalloc");
     if (rc != HMPC_OK) return rc;
-    if (!c->split_stream) {
-      if (hipStreamCreateWithFlags(&c->split_stream, hipStreamNonBlocking) != hipSuccess ||
-          hipEventCreateWithFlags(&c->split_fork, hipEventDisableTiming) != hipSuccess ||
-          hipEventCreateWithFlags(&c->split_join, hipEventDisableTiming) != hipSuccess) {
-        c->err = "split stream / events";
-        return HMPC_ERR_HIP;
-      }
-    }
+    rc = ensure_fork(c);
+    if (rc != HMPC_OK) return rc;
     a.split_count = c->ovf + 3;
     a.split_list = c->split;
     a.split_nbkt = c->N + 1;

@@ -1513,8 +1513,14 @@ __global__ void __launch_bounds__(RT) ric_overflow_kernel(SolveArgs a, int N) {
 // Each wave counts its 64 instances row by row: lane j < N reads C[i][j], one
 // coalesced row per load and a ballot (round 5; one thread per instance
 // walking its own row was 64 uncoalesced loads per instruction and 50 us per
-// N = 60 step at B = 4096).
-constexpr int kLptT = 256;
+// N = 60 step at B = 4096).  All 64 row loads are issued before
+// the first ballot, and a workgroup is one wave (B = 4096: 64 CUs, 64 atomics
+// per bucket counter): 9.3 us at N = 60 B = 4096, of which probe builds put
+// ~3.7 us on the C reads, ~1.6 us on the counters and ~4 us on the launch
+// itself (1024-thread groups: 78 us -- the per-CU load rate).  Run beside
+// the factorisation kernel on a second stream it saved nothing at N = 60
+// B = 4096 (1.597 vs 1.603 M, the fork / join costs what it hides).
+constexpr int kLptT = 64;
 constexpr int kLptMax = 13;
 static_assert(kRicNmax <= 64, "a C row per wave load");   // bucket counters in the overflow header (hmpc_capi.cpp)
 __global__ void __launch_bounds__(kLptT) ric_buckets_kernel(SolveArgs a, int N, int W) {
@@ -1526,24 +1532,19 @@ __global__ void __launch_bounds__(kLptT) ric_buckets_kernel(SolveArgs a, int N, 
   const int64_t i = i0 + lane;
   const bool in = i < a.B;
   int nst = 0;
-  // 16 rows per batch: all 16 loads issued before the first ballot (one
-  // round trip per batch; a load-ballot pair per row serialised them)
   const int64_t last = a.B - 1;
   const int col = lane < N ? lane : 0;
-#pragma unroll 1
-  for (int r0 = 0; r0 < 64; r0 += 16) {
-    double cv[16];
+  double cv[64];
 #pragma unroll
-    for (int u = 0; u < 16; ++u) {
-      const int64_t ir = i0 + r0 + u;
-      cv[u] = a.C[(ir < last ? ir : last) * a.C_bs + col];
-    }
+  for (int u = 0; u < 64; ++u) {
+    const int64_t ir = i0 + u;
+    cv[u] = a.C[(ir < last ? ir : last) * a.C_bs + col];
+  }
 #pragma unroll
-    for (int u = 0; u < 16; ++u) {
-      const bool ok = i0 + r0 + u <= last && lane < N;
-      const int cnt = __builtin_popcountll(__ballot(ok && cv[u] != 0.0));
-      nst = lane == r0 + u ? cnt : nst;
-    }
+  for (int u = 0; u < 64; ++u) {
+    const bool ok = i0 + u <= last && lane < N;
+    const int cnt = __builtin_popcountll(__ballot(ok && cv[u] != 0.0));
+    nst = lane == u ? cnt : nst;
   }
   const int k = in ? min(nst / W, nb - 1) : 0;
   uint64_t mine = 0;
@@ -1655,7 +1656,8 @@ bool ric_launch(int N, const SolveArgs& a, hipStream_t s, int* per) {
         return ric_launch_fac(ric_factor_kernel<VAR, 20, 38>, N, cap, a, s) &&
                ric_launch_k(ric_kernel<VAR, OCC, 20, 38, 2>, N, cap, a, s, per);
     }
-    return ric_launch_fac(ric_factor_kernel<VAR>, N, cap, a, s) && ric_launch_k(ric_kernel<VAR, OCC, 0, 0, 2>, N, cap, a, s, per);
+    return ric_launch_fac(ric_factor_kernel<VAR>, N, cap, a, s) &&
+           ric_launch_k(ric_kernel<VAR, OCC, 0, 0, 2>, N, cap, a, s, per);
   }
   if constexpr (OCC == 1) {
     if (ric_static_n(N) == 60) return ric_launch_k(ric_kernel<VAR, OCC, 60, 47>, N, cap, a, s, per);

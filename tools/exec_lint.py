@@ -6,7 +6,9 @@ divergent region's mask (empty after a divergent loop exits).  The copy then
 writes only the region's lanes; a lane outside it later reads a stale value.
 Only copies of a value that is live into the region (not written between
 the region's s_and_saveexec and the copy) are reported: those are needed by
-every lane.  (A heuristic over the text: straight-line distance, no CFG.)
+every lane; for an AGPR copy, only one read back after the restore (not a
+save / restore pair inside the region).  (A heuristic over the text:
+straight-line distance, no CFG.)
 
     python tools/exec_lint.py file.s ...            (hipcc --save-temps output)
     python tools/exec_lint.py --lib libhmpc.so      (disassembles the gfx950 code objects)
@@ -65,10 +67,38 @@ def _live_in(prog, i_copy, mask, src):
     return False
 
 
+AREG = re.compile(r'\ba(\d+)\b')
+AREAD = re.compile(r'^\s*v_accvgpr_read_b32\s+v\d+,\s*a(\d+)\b')
+AWRITE = re.compile(r'^\s*v_accvgpr_write_b32\s+a(\d+)\b')
+
+
+def _agpr_escapes(lines, k_copy, k_restore, areg):
+    """An AGPR copy is a hazard only if its value is used OUTSIDE the region:
+    not read back before the exec restore (a save / restore pair inside the
+    region is region-local), and read after the restore before it is
+    written again (straight-line scan to the kernel's end)."""
+    for _, ins in lines[k_copy + 1:k_restore]:
+        m = AREAD.match(ins)
+        if m and int(m.group(1)) == areg:
+            return False
+    for _, ins in lines[k_restore + 1:]:
+        if KERNEL.match(ins) and not ins.startswith('.LBB'):
+            return False
+        m = AREAD.match(ins)
+        if m and int(m.group(1)) == areg:
+            return True
+        m = AWRITE.match(ins)
+        if m and int(m.group(1)) == areg:
+            return False
+    return False
+
+
 def lint_lines(lines, where, precise=True):
     out = []
     kernel, block = '?', []
     prog = []   # (line, instruction) of the current kernel, in order
+    flat = [(ln, raw.split(';')[0].rstrip()) for ln, raw in lines]
+    pos = {ln: k for k, (ln, _) in enumerate(flat)}
     for ln, raw in lines:
         line = raw.split(';')[0].rstrip() if not raw.lstrip().startswith(';') else ''
         m = LABEL.match(raw)
@@ -87,8 +117,12 @@ def lint_lines(lines, where, precise=True):
                 if SPILL.match(bi):
                     ops = bi.strip().split(None, 1)[1]
                     src = _regs(ops.split(',')[1] if ops.startswith(('a', 'off')) or 'accvgpr' in bi else ops)
-                    if not precise or _live_in(prog, bidx, mask, src):
-                        out.append((where, kernel, bl, bi.strip()))
+                    if precise and not _live_in(prog, bidx, mask, src):
+                        continue
+                    ma = AWRITE.match(bi)
+                    if precise and ma and not _agpr_escapes(flat, pos[bl], pos[ln], int(ma.group(1))):
+                        continue
+                    out.append((where, kernel, bl, bi.strip()))
             block = []   # (later instructions run with the restored mask)
             prog.append((ln, line))
             continue

@@ -85,6 +85,10 @@ def main():
            'compacted': summary((nf <= cmp_nv) & ~sw), 'full': summary(nf > cmp_nv)}
     for s_ in np.unique(nst):
         res[f'stance{int(s_)}_nf{int(3 * N + (3 if var == "3f" else 2) * s_)}'] = summary(nst == s_)
+    # the slowest instances (the small-batch step is as long as its slowest one)
+    p99 = np.quantile(tot[stamped], 0.99) if stamped.any() else 0
+    res['slowest_1pct'] = summary(tot >= p99)
+    res['slowest_1pct']['nst_mean'] = float(nst[(tot >= p99) & stamped].mean()) if stamped.any() else 0.0
     # per-instance latency quantiles (s_memtime runs per XCD, so start times
     # of different instances are not comparable; latencies are)
     q = [0.0, 0.5, 0.9, 0.99, 1.0]

@@ -54,7 +54,7 @@ def pmc(cfgdir, main_token):
                 continue
             c, v = r['Counter_Name'], float(r['Counter_Value'])
             tot[(f, c)] += v
-            per_kernel[name.split('(')[0]][c] += v
+            per_kernel[name.replace('(anonymousnamespace)::', '').split('(')[0]][c] += v
             if main_token in name:
                 steps[f].add(r['Dispatch_Id'])
     out = {}
@@ -99,6 +99,24 @@ def main(tag, cfgs):
                 summary['valu_busy'] = m['SQ_ACTIVE_INST_VALU'] * 4 / (SIMDS * cyc)
             if 'SQ_WAVE_CYCLES' in m:
                 summary['resident_waves_per_simd'] = m['SQ_WAVE_CYCLES'] * 4 / (SIMDS * cyc)
+        # per kernel (PMC collection serialises the dispatches, so each kernel's
+        # GRBM_GUI_ACTIVE is its own duration): the split's classes one by one
+        dk = {}
+        for kn, kc in per_kernel.items():
+            kcyc = kc.get('GRBM_GUI_ACTIVE', 0.0) / XCDS
+            d = {}
+            if kcyc > 0 and 'SQ_ACTIVE_INST_VALU' in kc:
+                d['valu_busy'] = kc['SQ_ACTIVE_INST_VALU'] * 4 / (SIMDS * kcyc)
+            if kcyc > 0 and 'SQ_WAVE_CYCLES' in kc:
+                d['resident_waves_per_simd'] = kc['SQ_WAVE_CYCLES'] * 4 / (SIMDS * kcyc)
+            if kc.get('SQ_WAVE_CYCLES'):
+                d['wait_any_frac'] = kc.get('SQ_WAIT_ANY', 0) / kc['SQ_WAVE_CYCLES']
+                d['wait_inst_any_frac'] = kc.get('SQ_WAIT_INST_ANY', 0) / kc['SQ_WAVE_CYCLES']
+            if 'TCC_HIT_sum' in kc:
+                d['l2_hit_rate'] = kc['TCC_HIT_sum'] / max(1.0, kc['TCC_HIT_sum'] + kc['TCC_MISS_sum'])
+            if d:
+                dk[kn] = d
+        summary['derived_by_kernel'] = dk
         if 'TCC_HIT_sum' in m:
             summary['l2_hit_rate'] = m['TCC_HIT_sum'] / max(1.0, m['TCC_HIT_sum'] + m['TCC_MISS_sum'])
         entry = {'kernel': kernel, 'fp64_flops_executed_per_solve': f64 / B,
