@@ -382,29 +382,39 @@ __device__ __forceinline__ real tri_fwd_lds(real acc, const real* Mc, const real
   constexpr int SEND = L::W == 1 ? (NV + 3) & ~3 : ((NV + kRing2 - 1) / kRing2) * kRing2;   // padded (steps >= NV are no-ops)
   const int tid = threadIdx.x;
   if constexpr (L::W == 1) {
-    // M[tid][s] for tid > s sits at Mc[cb(s) + tid - s]; other lanes read a 0
-    // (the lane mask is built on the scalar unit: no v_cmp per step)
+    // M[tid][t] for tid > t sits at Mc[cb(t) + tid - t]; other lanes read a 0.
+    // Step t's lane mask (lanes t+1 .. NV-1) and address follow from step
+    // t-1's by a shift and an add (round 5: the per-step compare / select
+    // chain on the scalar unit was ~12 of the step's ~19 instructions, and a
+    // wave issues one instruction per 4 cycles).  Steps run in whole groups
+    // of kRing1 up to SE = nf rounded up: the columns nf .. SE-1 were zeroed
+    // after the Cholesky (sweep_pad_zero), the lanes >= nf hold 0.
     const unsigned base = lds_addr(Mc + tid), zaddr = lds_addr(zero);
     constexpr uint64_t kLive = NV >= 64 ? ~0ull : ((1ull << NV) - 1);
-    // (nf: the instance's free variables; steps >= nf are no-ops, their rows
-    // and columns are the identity)
-    auto addr = [&](int s) -> unsigned {
-      const uint64_t m = s < nf ? kLive & ~((2ull << s) - 1) : 0;   // lanes s+1 .. NV-1
-      return msel(m, base + (unsigned)RB * (unsigned)(L::cb(s) - s), zaddr);
-    };
+    auto mask = [&](int t) -> uint64_t { return t < NV - 1 ? kLive & ~((2ull << t) - 1) : 0; };
+    auto off = [&](int t) -> unsigned { return (unsigned)RB * (unsigned)(L::cb(t) - t); };
+    const int SE = (nf + kRing1 - 1) & ~(kRing1 - 1);
     real ring[kRing1];
     sfor<0, kRing1>([&](auto jc) __attribute__((always_inline)) {
-      lds_ld1(ring[decltype(jc)::value], addr(s0 + decltype(jc)::value));
+      constexpr int j = decltype(jc)::value;
+      lds_ld1(ring[j], msel(mask(s0 + j), base + off(s0 + j), zaddr));
     });
+    // the next ring refill: step t = s0 + kRing1
+    uint64_t mk = mask(s0 + kRing1);
+    unsigned ad = base + off(s0 + kRing1);
+    unsigned inc = (unsigned)RB * (unsigned)(NV - 1 - (s0 + kRing1));   // cb(t+1)-(t+1) - (cb(t)-t) = NV-1-t
 #pragma unroll 1
-    for (int s = s0; s < nf; s += kRing1) {   // (steps >= nf are no-ops)
+    for (int s = s0; s < SE; s += kRing1) {
       sfor<0, kRing1>([&](auto jc) __attribute__((always_inline)) {
         constexpr int j = decltype(jc)::value;
         const int sj = s + j;
         const real ys = rdlane(acc, sj);
         lds_wait<kRing1 - 1>(ring[j]);
         acc = fma(-ring[j], ys, acc);
-        lds_ld1(ring[j], addr(sj + kRing1));
+        lds_ld1(ring[j], msel(mk, ad, zaddr));
+        mk = (mk << 1) & kLive;
+        ad += inc;
+        inc -= (unsigned)RB;
       });
     }
     lds_drain(ring);   // the ring's last loads are dummies
@@ -459,32 +469,35 @@ template <class L>
 __device__ __forceinline__ real tri_bwd(real acc, const real* Mc, const real* zero,
                                           real dinv, real* red, int nf) {
   constexpr int NV = L::NV;
-  // first step, padded to the ring (steps >= nf are no-ops)
-  const int STOP = L::W == 1 ? ((nf + kRing1 - 1) & ~(kRing1 - 1)) - 1 : ((NV + 3) & ~3) - 1;
   const int tid = threadIdx.x;
   const int cbt = tid < NV ? L::cb(tid) : 0;
   acc *= dinv;
   if constexpr (L::W == 1) {
-    // M[s][tid] for tid < s sits at Mc[cbt + s - tid]; other lanes read a 0
-    // (the lane mask is built on the scalar unit: no v_cmp per step)
+    // M[t][tid] for tid < t sits at Mc[cbt + t - tid]; other lanes read a 0.
+    // From the last free step nf-1 down: step t's mask (lanes 0 .. t-1) is
+    // step t+1's shifted right, its address one entry lower (round 5, as in
+    // tri_fwd_lds).  The last group's steps below 0 read 0 on every lane.
     const unsigned base = lds_addr(Mc + cbt - tid), zaddr = lds_addr(zero);
-    auto addr = [&](int s) -> unsigned {
-      const uint64_t m = (s > 0 && s < nf) ? (1ull << s) - 1 : 0;   // lanes 0 .. s-1
-      return msel(m, base + (unsigned)RB * (unsigned)s, zaddr);
-    };
+    auto mask = [&](int t) -> uint64_t { return t > 0 ? (1ull << t) - 1 : 0; };
+    const int top = nf - 1;
     real ring[kRing1];
     sfor<0, kRing1>([&](auto jc) __attribute__((always_inline)) {
-      lds_ld1(ring[decltype(jc)::value], addr(STOP - decltype(jc)::value));
+      constexpr int j = decltype(jc)::value;
+      lds_ld1(ring[j], msel(mask(top - j), base + (unsigned)RB * (unsigned)(top - j), zaddr));
     });
+    uint64_t mk = mask(top - kRing1);   // the next ring refill: step top - kRing1
+    unsigned ad = base + (unsigned)RB * (unsigned)(top - kRing1);
 #pragma unroll 1
-    for (int s = STOP; s >= 0; s -= kRing1) {
+    for (int s = top; s >= 0; s -= kRing1) {
       sfor<0, kRing1>([&](auto jc) __attribute__((always_inline)) {
         constexpr int j = decltype(jc)::value;
         const int sj = s - j;
-        const real zs = rdlane(acc, sj);
+        const real zs = rdlane(acc, sj & 63);
         lds_wait<kRing1 - 1>(ring[j]);
         acc = fma(-ring[j], zs, acc);
-        lds_ld1(ring[j], addr(sj - kRing1));
+        lds_ld1(ring[j], msel(mk, ad, zaddr));
+        mk >>= 1;
+        ad -= (unsigned)RB;
       });
     }
     lds_drain(ring);   // the ring's last loads are dummies
@@ -1196,6 +1209,14 @@ solve_kernel(SolveArgs a) {
         // that let it do so returned wrong optima)
         if constexpr (k + 1 < NV) lds_wait<0>(nb[0], nb[1]);
       });
+      // sweep_pad_zero: columns nf .. nf+kRing1-2 of M were never stepped
+      // (stale LDS); zero them so the forward sweeps run whole ring groups
+      // past nf without a per-step bound (tri_fwd_lds)
+#pragma unroll
+      for (int c0 = 0; c0 < kRing1 - 1; ++c0) {
+        const int c = nf + c0;
+        if (c < NV && tid > c && tid < NV) sm[L::LC + L::cb(c) + tid - c] = real(0);
+      }
     } else {
       real mine = Rg[0];   // A[tid][k] of the current step
       // pivot extras (diag_extra) by lane, behind the column buffers (the
