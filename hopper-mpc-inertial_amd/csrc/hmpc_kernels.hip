@@ -223,7 +223,7 @@ struct Blk {
     }
   }
   __device__ __forceinline__ static void argmin(real& v, int& i, real* red) {
-    wave_argmin(v, i);
+    wave_argmin<true>(v, i);
     if constexpr (W > 1) {
       __syncthreads();
       if ((threadIdx.x & 63) == 0) {
@@ -557,10 +557,12 @@ __device__ __forceinline__ real tri_bwd(real acc, const real* Mc, const real* ze
 #define HMPC_TOC(slot, v) (stamp_[slot] += __builtin_amdgcn_s_memtime() - (v))
 #elif defined(HMPC_MARKS)   // phase markers in the .s (register-pressure work)
 #define HMPC_STAMP(i) asm volatile(";@@PHASE " #i)
+#define HMPC_TIC(v) asm volatile(";@@TIC " #v)
+#define HMPC_TOC(slot, v) asm volatile(";@@TOC " #slot)
 #else
 #define HMPC_STAMP(i) ((void)0)
 #endif
-#ifndef HMPC_STAMPS
+#if !defined(HMPC_STAMPS) && !defined(HMPC_MARKS)
 #define HMPC_TIC(v) ((void)0)
 #define HMPC_TOC(slot, v) ((void)0)
 #endif
@@ -1445,9 +1447,13 @@ solve_kernel(SolveArgs a) {
     const real sc2 = znorm > 0.0 ? zrow / znorm : ((zrow < -kTolR) ? -INFINITY : INFINITY);
     real best = INFINITY;
     int bid = 0x7fffffff;
-    if (nslots > 0 && !(actmask & 1)) argmin_combine(best, bid, sc0, 4 * tid);
-    if (nslots > 1 && !(actmask & 2)) argmin_combine(best, bid, sc1, 4 * tid + 1);
-    if (nslots > 2 && !(actmask & 4)) argmin_combine(best, bid, sc2, 4 * tid + 2);
+    {   // (selects: a slot that is not a candidate offers (inf, none))
+      const bool c0 = nslots > 0 && !(actmask & 1), c1 = nslots > 1 && !(actmask & 2);
+      const bool c2 = nslots > 2 && !(actmask & 4);
+      argmin_combine_sel(best, bid, c0 ? sc0 : real(INFINITY), c0 ? 4 * tid : 0x7fffffff);
+      argmin_combine_sel(best, bid, c1 ? sc1 : real(INFINITY), c1 ? 4 * tid + 1 : 0x7fffffff);
+      argmin_combine_sel(best, bid, c2 ? sc2 : real(INFINITY), c2 ? 4 * tid + 2 : 0x7fffffff);
+    }
     B::argmin(best, bid, red);
     HMPC_TOC(9, t_scan);
     if (!(best < -kTolR)) break;   // primal feasible: optimal
@@ -1507,11 +1513,17 @@ solve_kernel(SolveArgs a) {
       HMPC_TOC(12, t_bwd);
       HMPC_TIC(t_dual);
       // dual direction r = R^-1 c (lanes l < q), back substitution
+      // (the diagonal's reciprocals first, one division per lane off the
+      // substitution's chain, which is then readlane -> mul -> fma; the
+      // updates are selects, not exec-masked branches -- round 5)
       real rcur = tid < qu ? cbv[tid] : 0.0, rmine = 0.0;
+      const int td = tid < qu ? tid : 0;
+      const real rinv = real(1) / Rm[loff(td) + td];
       for (int l = qu - 1; l >= 0; --l) {
-        const real rl = B::bcast(rcur, l, red) / Rm[loff(l) + l];
-        if (tid == l) rmine = rl;
-        if (tid < l) rcur = fma(-Rm[loff(l) + tid], rl, rcur);
+        const real rl = B::bcast(rcur, l, red) * B::bcast(rinv, l, red);
+        const real rv = Rm[loff(l) + (tid < l ? tid : 0)];
+        rmine = (tid == l) ? rl : rmine;
+        rcur = (tid < l) ? fma(-rv, rl, rcur) : rcur;
       }
       // partial step length t1 (drop candidate)
       real t1 = INFINITY;
@@ -1740,6 +1752,8 @@ solve_kernel(SolveArgs a) {
       double objl = 0.0;
       const int nref = ka.refine;
       double lastdu = INFINITY;   // |du| of the last correction (no correction: not converged)
+      const int tq = tid < qu ? tid : 0;
+      const double rinv64 = 1.0 / (double)Rm[loff(tq) + tq];   // (R is fixed during the corrections)
       HMPC_TIC(t_ref);
 #pragma unroll 1
       for (int it = 0; it < nref; ++it) {
@@ -1784,19 +1798,21 @@ solve_kernel(SolveArgs a) {
           cvec = tid == l ? cl : cvec;
         });
         B::sync();
-        double tcur = r2, tmine = 0.0;   // t = R^-T r2
+        double tcur = r2, tmine = 0.0;   // t = R^-T r2 (reciprocals of R's diagonal: rinv64)
 #pragma unroll 1
         for (int l = 0; l < qu; ++l) {
-          const double tl = rdlane(tcur, l) / (double)Rm[loff(l) + l];
-          if (tid == l) tmine = tl;
-          if (tid > l && tid < qu) tcur = fma(-(double)Rm[loff(tid) + l], tl, tcur);
+          const double tl = rdlane(tcur, l) * rdlane(rinv64, l);
+          const double rv = (double)Rm[loff(tid > l && tid < qu ? tid : l) + l];
+          tmine = (tid == l) ? tl : tmine;
+          tcur = (tid > l && tid < qu) ? fma(-rv, tl, tcur) : tcur;
         }
         double rcur = tid < qu ? tmine - (double)cvec : 0.0, dlam = 0.0;   // dlam = R^-1 (t - c)
 #pragma unroll 1
         for (int l = qu - 1; l >= 0; --l) {
-          const double rl = rdlane(rcur, l) / (double)Rm[loff(l) + l];
-          if (tid == l) dlam = rl;
-          if (tid < l) rcur = fma(-(double)Rm[loff(l) + tid], rl, rcur);
+          const double rl = rdlane(rcur, l) * rdlane(rinv64, l);
+          const double rv = (double)Rm[loff(l) + (tid < l ? tid : 0)];
+          dlam = (tid == l) ? rl : dlam;
+          rcur = (tid < l) ? fma(-rv, rl, rcur) : rcur;
         }
         real zq = w;   // w - Qw c + Qw t
         ladder<0, QMAX>(qu, [&](auto lc) __attribute__((always_inline)) {
@@ -1911,6 +1927,10 @@ solve_kernel(SolveArgs a) {
     const real ubz = tid_o == 2 ? real(1) : real(0);
     const real gdt = tid_o == 8 ? -real(a.g) * dt : real(0);
     real objl = 0.0;
+    // the rollout first (x in registers), the objective after it: the x_ref
+    // loads issued above then land while the rollout runs instead of stalling
+    // its first stage (round 5)
+    real xk[N];
     sfor<0, N>([&](auto kc) __attribute__((always_inline)) {
       constexpr int k = decltype(kc)::value;
       const real cp = sm[L::CS + 2 * k], sp = sm[L::CS + 2 * k + 1];
@@ -1928,9 +1948,7 @@ solve_kernel(SolveArgs a) {
       }
       const real bu = (tid >= 9 && tid < 12) ? bw_u : ((tid >= 6 && tid < 9) ? bv_u : 0.0);
       xr = ad_lane(xr, dt, cp, sp) + bu + gdt;
-      const real kf = (k == N - 1) ? kTermQ : 1.0;
-      const real e = xr - xrg[k];
-      objl = fma(kf * qr * e, e, objl);
+      xk[k] = xr;
       if constexpr (k < N - 1) {
         const real ub = a.uref_aliased ? ((sm[L::CC + N - 1] != 0.0) ? 2.0 * a.m * a.g : 0.0)
                                          : ((sm[L::CC + k] != 0.0) ? 2.0 * a.m * a.g : 0.0);
@@ -1938,6 +1956,12 @@ solve_kernel(SolveArgs a) {
         objl = fma(rdu * du, du, objl);
       }
       if (tid < 12) xo[12 * (k + 1) + tid] = xr;
+    });
+    sfor<0, N>([&](auto kc) __attribute__((always_inline)) {
+      constexpr int k = decltype(kc)::value;
+      const real kf = (k == N - 1) ? kTermQ : 1.0;
+      const real e = xk[k] - xrg[k];
+      objl = fma(kf * qr * e, e, objl);
     });
     const real objv = B::sum(objl, red);
     __syncthreads();

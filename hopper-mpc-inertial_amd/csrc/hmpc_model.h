@@ -102,21 +102,34 @@ template <typename R>
 __device__ __forceinline__ void argmin_combine(R& v, int& i, R v2, int i2) {
   if (v2 < v || (v2 == v && i2 < i)) { v = v2; i = i2; }
 }
+// the same, branch-free (selects, not an exec-masked branch per combine:
+// the dense kernels, round 5; the Riccati kernels keep the branch form,
+// which their register allocation at the 2-wave cap is tuned to)
+template <typename R>
+__device__ __forceinline__ void argmin_combine_sel(R& v, int& i, R v2, int i2) {
+  const bool take = (v2 < v) | ((v2 == v) & (i2 < i));
+  v = take ? v2 : v;
+  i = take ? i2 : i;
+}
 
 // (min v, its smallest i) over the wave, wave-uniform; the same row butterfly
 // + readlane shape as wave_sum.  Lexicographic (v, i) minimum: independent of
 // the combining order.
-template <typename R>
+template <bool SEL = false, typename R>
 __device__ __forceinline__ void wave_argmin(R& v, int& i) {
-  argmin_combine(v, i, dpp<kDppXor1>(v), dpp<kDppXor1>(i));
-  argmin_combine(v, i, dpp<kDppXor2>(v), dpp<kDppXor2>(i));
-  argmin_combine(v, i, dpp<kDppHalfMirror>(v), dpp<kDppHalfMirror>(i));
-  argmin_combine(v, i, dpp<kDppMirror>(v), dpp<kDppMirror>(i));
+  auto comb = [](R& a, int& ia, R b, int ib) __attribute__((always_inline)) {
+    if constexpr (SEL) argmin_combine_sel(a, ia, b, ib);
+    else argmin_combine(a, ia, b, ib);
+  };
+  comb(v, i, dpp<kDppXor1>(v), dpp<kDppXor1>(i));
+  comb(v, i, dpp<kDppXor2>(v), dpp<kDppXor2>(i));
+  comb(v, i, dpp<kDppHalfMirror>(v), dpp<kDppHalfMirror>(i));
+  comb(v, i, dpp<kDppMirror>(v), dpp<kDppMirror>(i));
   R vb = rdlane(v, 0);
   int ib = __builtin_amdgcn_readlane(i, 0);
-  argmin_combine(vb, ib, rdlane(v, 16), __builtin_amdgcn_readlane(i, 16));
-  argmin_combine(vb, ib, rdlane(v, 32), __builtin_amdgcn_readlane(i, 32));
-  argmin_combine(vb, ib, rdlane(v, 48), __builtin_amdgcn_readlane(i, 48));
+  comb(vb, ib, rdlane(v, 16), __builtin_amdgcn_readlane(i, 16));
+  comb(vb, ib, rdlane(v, 32), __builtin_amdgcn_readlane(i, 32));
+  comb(vb, ib, rdlane(v, 48), __builtin_amdgcn_readlane(i, 48));
   v = vb;
   i = ib;
 }

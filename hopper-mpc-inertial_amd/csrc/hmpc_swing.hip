@@ -992,6 +992,9 @@ __global__ void __launch_bounds__(64, HMPC_SWING_WAVES) swing_kernel(SolveArgs a
     const double gdt = hl == 8 ? -a.g * dt : 0.0;
     const double isw = (hl >= 9 && hl < 12) ? 1.0 : 0.0;
     double objl = 0.0;
+    // the rollout first, the objective after it: the x_ref loads land while
+    // the rollout runs (as in the dense kernel's phase 7)
+    double xk[N];
     sfor<0, N>([&](auto kc) __attribute__((always_inline)) {
       constexpr int k = decltype(kc)::value;
       const double cp = sm[L::CS + 2 * k], sp = sm[L::CS + 2 * k + 1];
@@ -1001,14 +1004,18 @@ __global__ void __launch_bounds__(64, HMPC_SWING_WAVES) swing_kernel(SolveArgs a
 #pragma unroll
       for (int c = 0; c < 3; ++c) bw_u = fma(bwr[c], uk[c], bw_u);
       xr = ad_lane_h(xr, dt, cp, sp, hl) + isw * bw_u + gdt;
-      const double kf = (k == N - 1) ? kTermQ : 1.0;
-      const double e = xr - xrg[k];
-      objl = fma(kf * qr * e, e, objl);
+      xk[k] = xr;
       if constexpr (k < N - 1) {
         const double du = uk[tu];
         objl = fma(rdu * du, du, objl);
       }
       if (hl < 12) xo[12 * (k + 1) + hl] = xr;
+    });
+    sfor<0, N>([&](auto kc) __attribute__((always_inline)) {
+      constexpr int k = decltype(kc)::value;
+      const double kf = (k == N - 1) ? kTermQ : 1.0;
+      const double e = xk[k] - xrg[k];
+      objl = fma(kf * qr * e, e, objl);
     });
     const double objv = half_sum(objl);
     wsync();
