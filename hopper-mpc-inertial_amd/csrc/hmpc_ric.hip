@@ -1111,8 +1111,16 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
         }
         yv[e] = cvl;
       }
+      // the reciprocals of R's diagonal first (one division per lane), so the
+      // substitutions' chains are readlane -> mul -> fma (round 5)
+      double rinv[ENT];
+#pragma unroll
+      for (int e = 0; e < ENT; ++e) {
+        const int m = 64 * e + lane < q ? 64 * e + lane : 0;
+        rinv[e] = 1.0 / Rm[loff(m) + m];
+      }
       for (int l = 0; l < q; ++l) {   // forward substitution with R'
-        const double yl = vget(yv, l) / Rm[loff(l) + l];
+        const double yl = vget(yv, l) * vget(rinv, l);
         vset(yv, l, yl);
 #pragma unroll
         for (int e = 0; e < ENT; ++e) {
@@ -1123,7 +1131,7 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
 #pragma unroll
       for (int e = 0; e < ENT; ++e) rv[e] = yv[e];
       for (int l = q - 1; l >= 0; --l) {   // back substitution with R
-        const double rl = vget(rv, l) / Rm[loff(l) + l];
+        const double rl = vget(rv, l) * vget(rinv, l);
         vset(rv, l, rl);
 #pragma unroll
         for (int e = 0; e < ENT; ++e) {
