@@ -70,8 +70,11 @@ __device__ __forceinline__ float row_shift(float x) {
 
 // DPP lane permutes within a row of 16 lanes (VALU modifiers: no LDS round
 // trip, unlike the bpermute behind __shfl_xor).
+// (mov_dpp: no "old" operand -- every control used here reads a valid lane of
+// the row, so the old value was never selected, but update_dpp(0, ...) made
+// the compiler materialise the 0 in two v_movs per 64-bit permute)
 template <int CTRL>
-__device__ __forceinline__ int dpp(int x) { return __builtin_amdgcn_update_dpp(0, x, CTRL, 0xf, 0xf, false); }
+__device__ __forceinline__ int dpp(int x) { return __builtin_amdgcn_mov_dpp(x, CTRL, 0xf, 0xf, false); }
 template <int CTRL>
 __device__ __forceinline__ double dpp(double x) {
   const long long b = __double_as_longlong(x);
