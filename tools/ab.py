@@ -43,8 +43,13 @@ def main():
     res = {lab: [] for _, _, lab in variants}
     for r in range(a.rounds):
         for lib, extra, lab in variants:
-            path = lib if os.path.isabs(lib) else os.path.join(ROOT, 'hopper-mpc-inertial_amd', lib)
+            # "libhmpc.so:NAME=VALUE,..." runs the library with those environment variables
+            libname, _, envs = lib.partition(':')
+            path = libname if os.path.isabs(libname) else os.path.join(ROOT, 'hopper-mpc-inertial_amd', libname)
             env = dict(os.environ, HMPC_LIB=path)
+            for kv in filter(None, envs.split(',')):
+                k, _, v = kv.partition('=')
+                env[k] = v
             cmd = ['timeout', '-k', '10', str(a.timeout), sys.executable, os.path.join(ROOT, 'bench.py'),
                    '--cpu-seconds', '0'] + a.args.split() + extra
             p = subprocess.run(cmd, env=env, capture_output=True, text=True, cwd=ROOT)
