@@ -5,8 +5,9 @@ N = 10) at B = 4096 of the bench workload, every instance against the C port
 reference-built problem data): equal statuses, |du| <= 1e-6, objective
 1e-9 relative, x* 1e-6.  B = 4096 takes the longest-first class order
 (hmpc_set_order auto); B = 16384 of configs[2] the index order, so both
-dense-split launch forms (bucket lists and plain class lists, each with the
-all-swing class) are covered.  Reference: src/mpc_cvx_euler_3f.py:96-160,
+dense-split launch forms (bucket lists and plain class lists) are covered, and
+B = 32768 the swing-first launch (the all-swing class before the full class
+on the caller's stream, HMPC_SWING_FIRST_B).  Reference: src/mpc_cvx_euler_3f.py:96-160,
 src/mpc_cvx_euler_2f.py:96-158."""
 import numpy as np
 import pytest
@@ -25,7 +26,8 @@ def hm():
 
 
 @pytest.mark.parametrize('variant,curve,B,order', [('3f', True, 4096, 'auto'), ('3f', True, 16384, 'auto'),
-                                                   ('3f', True, 4096, 'index'), ('2f', False, 4096, 'auto')])
+                                                   ('3f', True, 4096, 'index'), ('2f', False, 4096, 'auto'),
+                                                   ('3f', True, 32768, 'auto')])
 def test_config_vs_port(hm, variant, curve, B, order):
     import hmpc_plan
     from oracle import port
