@@ -2161,10 +2161,6 @@ bool HMPC_CAT(HMPC_CAT(launch_solve_n, HMPC_INST_N), HMPC_LAUNCH_SUFFIX)(int var
 #else
     constexpr bool kSw = false;
 #endif
-    // (A/B knobs, read once: HMPC_SPLIT_ORDER=1 full class first at every
-    // size; HMPC_LPT_SWING=1 the swing class in the longest-first order too)
-    static const int ord = [] { const char* e = getenv("HMPC_SPLIT_ORDER"); return e ? atoi(e) : 0; }();
-    static const int lsw = kSw ? [] { const char* e = getenv("HMPC_LPT_SWING"); return e ? atoi(e) : 0; }() : 0;
     SolveArgs as = af;   // the all-swing class (kSw): list 2, or bucket 0
     as.list = a.split_list + 2 * a.B;
     as.list_count = a.split_count + 2;
@@ -2177,7 +2173,7 @@ bool HMPC_CAT(HMPC_CAT(launch_solve_n, HMPC_INST_N), HMPC_LAUNCH_SUFFIX)(int var
       // order at B = 4096 it cost 8-12 %, configs[1] 24.3 -> 22.3 M, since
       // those windows are the cheapest and fill the tail as bucket 0 of the
       // compacted class; profiles/r05_ab.json)
-      ac.lpt_lo = lsw ? 1 : 0;   // (bucket 0 to the swing class with HMPC_LPT_SWING)
+      ac.lpt_lo = 0;
       ac.lpt_hi = smax;
       af.lpt_lo = smax + 1;
       af.lpt_hi = N;
@@ -2203,6 +2199,9 @@ bool HMPC_CAT(HMPC_CAT(launch_solve_n, HMPC_INST_N), HMPC_LAUNCH_SUFFIX)(int var
     //   split stream -- configs[2] (B = 65536) 57.0 -> 58.8 M solves/s;
     //   otherwise full on the caller's stream, swing then compacted on the split
     //   stream -- B = 16384 45.5 vs 42.1 M, configs[1] 22.3 vs 18.5 M.
+    // Re-measured at round end (r05_knob_*): full first at B = 65536 62.6 vs
+    // 63.8 M; the swing class in the longest-first order costs 10-12 % at
+    // B = 4096 (28.4 -> 25.6 M at configs[1]) and nothing at 8192.
     auto full_on = [&](hipStream_t st) {
       if (variant == 3) hipLaunchKernelGGL((solve_kernel<3, N, real>), dim3((unsigned)a.B), dim3(NT), HMPC_DIAG_LDS_FULL, st, af);
 #ifdef HMPC_FULL2F_NV
@@ -2220,13 +2219,13 @@ bool HMPC_CAT(HMPC_CAT(launch_solve_n, HMPC_INST_N), HMPC_LAUNCH_SUFFIX)(int var
 #ifndef HMPC_SWING_FIRST_B
 #define HMPC_SWING_FIRST_B 32768
 #endif
-    if (kSw && !a.lpt && a.B >= HMPC_SWING_FIRST_B && ord == 0) {
+    if (kSw && !a.lpt && a.B >= HMPC_SWING_FIRST_B) {
       swing_on(s);
       full_on(s);
       cmp_on(s2);
     } else {
       full_on(s);
-      if (!a.lpt || lsw) swing_on(s2);
+      if (!a.lpt) swing_on(s2);
       cmp_on(s2);
     }
     if (s2 != s) {
