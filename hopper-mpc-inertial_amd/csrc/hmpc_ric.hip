@@ -953,6 +953,14 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
     const double vz = zdot(vv);
     double best = INFINITY;
     int bid = 0x7fffffff;
+    // the one-wave main-pass kernels (N > 24; register room) combine by
+    // selects, not exec-masked branches (round 5); the 2-wave kernels keep the
+    // branch form their register allocation is tuned to
+    constexpr bool kSel = RING != 2 && ENT == 1;
+    auto comb = [&](bool c, double v, int i) __attribute__((always_inline)) {
+      if constexpr (kSel) argmin_combine_sel(best, bid, c ? v : INFINITY, c ? i : 0x7fffffff);
+      else if (c) argmin_combine(best, bid, v, i);
+    };
     if (lane < N) {
       const int k = lane;
       double u[6];
@@ -962,31 +970,31 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
       for (int c = 3; c < 6; ++c) {
         const double lim = tau_lim(c);
         const int v = 6 * k + c;
-        if (!(amask & (1 << (4 * c)))) argmin_combine(best, bid, u[c] + lim, 4 * v);
-        if (!(amask & (1 << (4 * c + 1)))) argmin_combine(best, bid, lim - u[c], 4 * v + 1);
+        comb(!(amask & (1 << (4 * c))), u[c] + lim, 4 * v);
+        comb(!(amask & (1 << (4 * c + 1))), lim - u[c], 4 * v + 1);
       }
-      if (k >= 2 && !(amask & (1 << 14))) {
+      if (k >= 2) {
         const double zrow = (zb[k] - kZmin) + vz;
         const double zn = znrm[k];
         const double s2 = zn > 0.0 ? zrow / zn : ((zrow < -kTol) ? -INFINITY : INFINITY);
-        argmin_combine(best, bid, s2, 4 * (6 * k + 3) + 2);
+        comb(!(amask & (1 << 14)), s2, 4 * (6 * k + 3) + 2);
       }
       if (stance_me) {
         const int v = 6 * k + 2;
-        if (!(amask & (1 << 8))) argmin_combine(best, bid, u[2], 4 * v);
-        if (!(amask & (1 << 9))) argmin_combine(best, bid, kFzMax - u[2], 4 * v + 1);
+        comb(!(amask & (1 << 8)), u[2], 4 * v);
+        comb(!(amask & (1 << 9)), kFzMax - u[2], 4 * v + 1);
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
           if (VAR == 2 && c == 1) continue;
           const int vc = 6 * k + c;
-          if (!(amask & (1 << (4 * c)))) argmin_combine(best, bid, (mu * u[2] - u[c]) * inv01, 4 * vc);
-          if (!(amask & (1 << (4 * c + 1)))) argmin_combine(best, bid, (mu * u[2] + u[c]) * inv01, 4 * vc + 1);
+          comb(!(amask & (1 << (4 * c))), (mu * u[2] - u[c]) * inv01, 4 * vc);
+          comb(!(amask & (1 << (4 * c + 1))), (mu * u[2] + u[c]) * inv01, 4 * vc + 1);
         }
       }
     }
     [[maybe_unused]] const double lbest = best;   // this stage's most violated (MRHS candidates)
     [[maybe_unused]] const int lbid = bid;
-    wave_argmin(best, bid);
+    wave_argmin<kSel>(best, bid);
     RS_ACC(4, t_scan);
     if (!(best < -kTol)) break;   // primal feasible: optimal
     RS_T(t_s);
@@ -1022,7 +1030,7 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
         for (int r = 1; r < kMRK; ++r) {
           double b2 = bl;
           int i2 = lbid;
-          wave_argmin(b2, i2);
+          wave_argmin<RING != 2 && ENT == 1>(b2, i2);
           if (!(b2 < -kTol)) break;
           const int q2 = uni(i2);
           if (lbid == q2) bl = INFINITY;
@@ -1119,13 +1127,20 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
         const int m = 64 * e + lane < q ? 64 * e + lane : 0;
         rinv[e] = 1.0 / Rm[loff(m) + m];
       }
+      constexpr bool kSelU = RING != 2 && ENT == 1;   // (selects in the one-wave kernels, as the scan)
       for (int l = 0; l < q; ++l) {   // forward substitution with R'
         const double yl = vget(yv, l) * vget(rinv, l);
         vset(yv, l, yl);
 #pragma unroll
         for (int e = 0; e < ENT; ++e) {
           const int m = 64 * e + lane;
-          if (m > l && m < q) yv[e] = fma(-Rm[loff(m) + l], yl, yv[e]);
+          if constexpr (kSelU) {
+            const bool up = m > l && m < q;
+            const double rv_ = Rm[loff(up ? m : l) + l];
+            yv[e] = up ? fma(-rv_, yl, yv[e]) : yv[e];
+          } else if (m > l && m < q) {
+            yv[e] = fma(-Rm[loff(m) + l], yl, yv[e]);
+          }
         }
       }
 #pragma unroll
@@ -1136,7 +1151,12 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
 #pragma unroll
         for (int e = 0; e < ENT; ++e) {
           const int m = 64 * e + lane;
-          if (m < l) rv[e] = fma(-Rm[loff(l) + m], rl, rv[e]);
+          if constexpr (kSelU) {
+            const double r_ = Rm[loff(l) + (m < l ? m : 0)];
+            rv[e] = m < l ? fma(-r_, rl, rv[e]) : rv[e];
+          } else if (m < l) {
+            rv[e] = fma(-Rm[loff(l) + m], rl, rv[e]);
+          }
         }
       }
       // z = H^-1 (n_p - N_A r), n_z' z
@@ -1251,9 +1271,14 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
 #pragma unroll
       for (int e = 0; e < ENT; ++e) {
         const int ai = 64 * e + lane;
-        if (ai < q && rv[e] > 0.0) argmin_combine(t1, kdrop, ua[ai] / rv[e], ai);
+        if constexpr (RING != 2 && ENT == 1) {
+          const bool c = ai < q && rv[e] > 0.0;
+          argmin_combine_sel(t1, kdrop, c ? ua[ai < q ? ai : 0] / rv[e] : INFINITY, c ? ai : 0x7fffffff);
+        } else if (ai < q && rv[e] > 0.0) {
+          argmin_combine(t1, kdrop, ua[ai] / rv[e], ai);
+        }
       }
-      wave_argmin(t1, kdrop);
+      wave_argmin<RING != 2 && ENT == 1>(t1, kdrop);
       // full step t2
       const double sp_ = cdot(p, vv, zdot(vv)) - bp;
       const bool has_z = zn > 1e-12 * sn;
