@@ -953,10 +953,10 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
     const double vz = zdot(vv);
     double best = INFINITY;
     int bid = 0x7fffffff;
-    // the one-wave main-pass kernels (N > 24; register room) combine by
-    // selects, not exec-masked branches (round 5); the 2-wave kernels keep the
-    // branch form their register allocation is tuned to
-    constexpr bool kSel = RING != 2 && ENT == 1;
+    // the main-pass kernels combine by selects, not exec-masked branches
+    // (round 5: N = 60 +3 %, configs[3] +1.7 %, less scratch at the 2-wave
+    // cap); the overflow pass (ENT > 1) keeps the branch form
+    constexpr bool kSel = ENT == 1;
     auto comb = [&](bool c, double v, int i) __attribute__((always_inline)) {
       if constexpr (kSel) argmin_combine_sel(best, bid, c ? v : INFINITY, c ? i : 0x7fffffff);
       else if (c) argmin_combine(best, bid, v, i);
@@ -1030,7 +1030,7 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
         for (int r = 1; r < kMRK; ++r) {
           double b2 = bl;
           int i2 = lbid;
-          wave_argmin<RING != 2 && ENT == 1>(b2, i2);
+          wave_argmin<ENT == 1>(b2, i2);
           if (!(b2 < -kTol)) break;
           const int q2 = uni(i2);
           if (lbid == q2) bl = INFINITY;
@@ -1127,7 +1127,7 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
         const int m = 64 * e + lane < q ? 64 * e + lane : 0;
         rinv[e] = 1.0 / Rm[loff(m) + m];
       }
-      constexpr bool kSelU = RING != 2 && ENT == 1;   // (selects in the one-wave kernels, as the scan)
+      constexpr bool kSelU = ENT == 1;   // (selects in the main-pass kernels, as the scan)
       for (int l = 0; l < q; ++l) {   // forward substitution with R'
         const double yl = vget(yv, l) * vget(rinv, l);
         vset(yv, l, yl);
@@ -1271,14 +1271,14 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
 #pragma unroll
       for (int e = 0; e < ENT; ++e) {
         const int ai = 64 * e + lane;
-        if constexpr (RING != 2 && ENT == 1) {
+        if constexpr (ENT == 1) {
           const bool c = ai < q && rv[e] > 0.0;
           argmin_combine_sel(t1, kdrop, c ? ua[ai < q ? ai : 0] / rv[e] : INFINITY, c ? ai : 0x7fffffff);
         } else if (ai < q && rv[e] > 0.0) {
           argmin_combine(t1, kdrop, ua[ai] / rv[e], ai);
         }
       }
-      wave_argmin<RING != 2 && ENT == 1>(t1, kdrop);
+      wave_argmin<ENT == 1>(t1, kdrop);
       // full step t2
       const double sp_ = cdot(p, vv, zdot(vv)) - bp;
       const bool has_z = zn > 1e-12 * sn;
