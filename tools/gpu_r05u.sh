@@ -1,7 +1,7 @@
 # round 5 end: the driver's round-end sequence on the final tree -- GPU suite,
 # smoke(), the default bench line
 set -o pipefail
-O=gpurun_out/r05u
+O=gpurun_out/r05final
 mkdir -p $O
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/tests.log 2>&1; rc=$?; tail -3 $O/tests.log
 [ $rc -eq 0 ] || exit 1
