@@ -45,6 +45,7 @@ struct hmpc_ctx {
   // the counters need a zeroing before the next solve (fresh buffer, or a
   // solve whose overflow pass -- which zeroes them at its end -- did not run)
   bool ovf_dirty = true;
+  bool ovf_total_failed = false;   // the diagnostic counter could not be allocated
   double* rws = nullptr;
   // dense split launch: the three class lists [3][split_cap], or (longest-first
   // order) up to N + 1 stance-count buckets of split_cap entries; the Riccati
@@ -256,12 +257,17 @@ int prepare_ric(hmpc_ctx* c, int64_t B, hmpc::SolveArgs& a) {
   a.ovf_count = c->ovf;
   a.work = c->ovf + 1;
   a.ovf_list = c->ovf + kOvfHeader;
-  if (!c->ovf_total) {
+  if (!c->ovf_total && !c->ovf_total_failed) {
+    // a diagnostic counter: zeroed and synchronised once at allocation (the
+    // null-stream memset is then ordered before any solve stream's kernel),
+    // and a failed allocation leaves it unavailable rather than failing the
+    // solve
     if (hipMalloc(&c->ovf_total, sizeof(unsigned long long)) != hipSuccess ||
-        hipMemset(c->ovf_total, 0, sizeof(unsigned long long)) != hipSuccess) {
+        hipMemset(c->ovf_total, 0, sizeof(unsigned long long)) != hipSuccess ||
+        hipDeviceSynchronize() != hipSuccess) {
+      if (c->ovf_total) (void)hipFree(c->ovf_total);
       c->ovf_total = nullptr;
-      c->err = "overflow total hipMalloc";
-      return HMPC_ERR_NOMEM;
+      c->ovf_total_failed = true;
     }
   }
   a.ovf_total = c->ovf_total;

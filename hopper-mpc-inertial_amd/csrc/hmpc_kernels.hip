@@ -77,8 +77,7 @@ constexpr bool kRefine = kF32 && HMPC_F32_REFINE;
 constexpr double kRefineTol = 1e-9;
 // and the largest last correction accepted as converged
 constexpr double kRefineDu = 4e-6;
-// ... and the early exit of the corrections (HMPC_REFINE_NO_EARLY_EXIT: always
-// a.refine of them)
+// ... and the early exit of the corrections
 constexpr double kRefineStop = 4e-7;
 // feasibility tolerance of the slack scan and the relative threshold on
 // |w_perp|^2 for a usable primal direction, per precision
@@ -389,6 +388,10 @@ __device__ __forceinline__ real tri_fwd_lds(real acc, const real* Mc, const real
     // wave issues one instruction per 4 cycles).  Steps run in whole groups
     // of kRing1 up to SE = nf rounded up: the columns nf .. SE-1 were zeroed
     // after the Cholesky (sweep_pad_zero), the lanes >= nf hold 0.
+    // whole ring groups from s0 on: only columns nf .. nf+kRing1-2 are
+    // zeroed past nf (sweep_pad_zero), so s0 is held to a group boundary here
+    // rather than trusted from the caller
+    s0 &= ~(kRing1 - 1);
     const unsigned base = lds_addr(Mc + tid), zaddr = lds_addr(zero);
     constexpr uint64_t kLive = NV >= 64 ? ~0ull : ((1ull << NV) - 1);
     auto mask = [&](int t) -> uint64_t { return t < NV - 1 ? kLive & ~((2ull << t) - 1) : 0; };
@@ -492,7 +495,10 @@ __device__ __forceinline__ real tri_bwd(real acc, const real* Mc, const real* ze
       sfor<0, kRing1>([&](auto jc) __attribute__((always_inline)) {
         constexpr int j = decltype(jc)::value;
         const int sj = s - j;
-        const real zs = rdlane(acc, sj & 63);
+        // (steps below 0 of the last group read lane 0, a free variable's
+        // finite value, times the 0 loaded from zaddr -- not a padding lane,
+        // whose value need not be finite: ADVICE r5)
+        const real zs = rdlane(acc, sj > 0 ? sj : 0);
         lds_wait<kRing1 - 1>(ring[j]);
         acc = fma(-ring[j], zs, acc);
         lds_ld1(ring[j], msel(mk, ad, zaddr));
@@ -1825,11 +1831,9 @@ solve_kernel(SolveArgs a) {
         lam += dlam;
         if (active_lane) dlo[L::DU + fidx] = u64;
         B::sync();
-#ifndef HMPC_REFINE_NO_EARLY_EXIT
         // converged: a correction below kRefineStop on every lane leaves an
         // error <= 0.25 x kRefineStop = 1e-7 (contraction <= cond x eps32 <= 0.2)
         if (!__ballot(lastdu > kRefineStop)) break;
-#endif
       }
       HMPC_TOC(15, t_ref);
       // outputs: x* (staged over L, dead now) and the objective from an fp64
@@ -2090,14 +2094,6 @@ __global__ void __launch_bounds__(kClsT) classify_kernel(SolveArgs a) {
 #ifndef HMPC_LAUNCH_SUFFIX
 #define HMPC_LAUNCH_SUFFIX
 #endif
-// diagnostic builds (tools/phase_stamps.py): dynamic LDS added to the class
-// launches to hold residency down (16 / 24 KB: one wave per SIMD)
-#ifndef HMPC_DIAG_LDS_FULL
-#define HMPC_DIAG_LDS_FULL 0
-#endif
-#ifndef HMPC_DIAG_LDS_CMP
-#define HMPC_DIAG_LDS_CMP 0
-#endif
 #if defined(HMPC_CMP_NV) && HMPC_CMP_NV > 0
 // the split's compacted kernel launches from a translation unit of its own
 // (-DHMPC_CMP_ONLY): the objects build in parallel
@@ -2125,16 +2121,16 @@ int HMPC_CAT(swing_qmax_n, HMPC_INST_N)();
 bool HMPC_CMP_LAUNCH(int variant, const SolveArgs& a, hipStream_t s) {
   if (variant == 3)
     hipLaunchKernelGGL((solve_kernel<3, HMPC_INST_N, real, HMPC_CMP_NV, HMPC_CMP_Q>), dim3((unsigned)a.B), dim3(64),
-                       HMPC_DIAG_LDS_CMP, s, a);
+                       0, s, a);
   else
     hipLaunchKernelGGL((solve_kernel<2, HMPC_INST_N, real, HMPC_CMP_NV, HMPC_CMP_Q>), dim3((unsigned)a.B), dim3(64),
-                       HMPC_DIAG_LDS_CMP, s, a);
+                       0, s, a);
   return true;
 }
 #ifdef HMPC_FULL2F_NV
 bool HMPC_FULL2F_LAUNCH(const SolveArgs& a, hipStream_t s) {
   hipLaunchKernelGGL((solve_kernel<2, HMPC_INST_N, real, HMPC_FULL2F_NV, HMPC_FULL2F_Q>), dim3((unsigned)a.B), dim3(64),
-                     HMPC_DIAG_LDS_FULL, s, a);
+                     0, s, a);
   return true;
 }
 #endif
@@ -2203,7 +2199,7 @@ bool HMPC_CAT(HMPC_CAT(launch_solve_n, HMPC_INST_N), HMPC_LAUNCH_SUFFIX)(int var
     // 63.8 M; the swing class in the longest-first order costs 10-12 % at
     // B = 4096 (28.4 -> 25.6 M at configs[1]) and nothing at 8192.
     auto full_on = [&](hipStream_t st) {
-      if (variant == 3) hipLaunchKernelGGL((solve_kernel<3, N, real>), dim3((unsigned)a.B), dim3(NT), HMPC_DIAG_LDS_FULL, st, af);
+      if (variant == 3) hipLaunchKernelGGL((solve_kernel<3, N, real>), dim3((unsigned)a.B), dim3(NT), 0, st, af);
 #ifdef HMPC_FULL2F_NV
       else HMPC_FULL2F_LAUNCH(af, st);
 #else

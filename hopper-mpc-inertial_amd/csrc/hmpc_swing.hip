@@ -763,12 +763,6 @@ __global__ void __launch_bounds__(64, HMPC_SWING_WAVES) swing_kernel(SolveArgs a
   // ---------------- phase 5: v0 = -L^-T L^-1 h --------------------------------
   double v = tri_bwd<L>(wv * dinv, bbase, zaddr, dinv);
   SW_STAMP(6);
-#ifdef HMPC_SWING_DEBUG
-  // (debug build, tools/swing_debug3.py: per lane v0, the first w and z, and
-  // scalars of the first inner iteration, written over x*)
-  double dbg0 = v, dbg1 = 0.0, dbg2 = 0.0, dbg3 = 0.0;
-  int dbg_n = 0;
-#endif
   // (padding lanes hold 0: zero rows and right-hand sides)
 
   // ---------------- phase 6: Goldfarb-Idnani, range-space form --------------
@@ -811,13 +805,6 @@ __global__ void __launch_bounds__(64, HMPC_SWING_WAVES) swing_kernel(SolveArgs a
     const double wfull = tri_fwd<L>(np_me, fbase, zaddr, dinv);
     const double wnorm2 = half_sum(wfull * wfull);
     SW_TOC(10, t_fwd);
-#ifdef HMPC_SWING_DEBUG
-    if (dbg_n == 0) {
-      dbg1 = wfull;
-      if (hl == 0) dbg3 = p;
-      if (hl == 1) dbg3 = wnorm2;
-    }
-#endif
     // ---- inner loop: step towards satisfying constraint p ----
     while (true) {
       if (++iters > max_iter) { status = ST_MAXIT; done = true; break; }
@@ -862,19 +849,6 @@ __global__ void __launch_bounds__(64, HMPC_SWING_WAVES) swing_kernel(SolveArgs a
       const bool has_z = zn > 1e-24 * wnorm2;
       const double t2 = has_z ? -sp_ / zn : INFINITY;
       const double t = t1 < t2 ? t1 : t2;
-#ifdef HMPC_SWING_DEBUG
-      if (dbg_n == 0) {
-        dbg2 = zi;
-        if (hl == 2) dbg3 = t1;
-        if (hl == 3) dbg3 = t2;
-        if (hl == 4) dbg3 = sp_;
-        if (hl == 5) dbg3 = zn;
-        if (hl == 6) dbg3 = qu;
-        if (hl == 7) dbg3 = bp;
-      }
-      if (hl == 8 + dbg_n && dbg_n < 20) dbg3 = p + 1000 * (has_z && t == t2 ? 1 : 0) + 10000 * qu;
-      ++dbg_n;
-#endif
       if (!(t < INFINITY)) { status = ST_INFEAS; done = true; break; }
       if (has_z) v = fma(t, zi, v);
       if (hl < qu) ua[hl] -= t * rmine;
@@ -1019,14 +993,6 @@ __global__ void __launch_bounds__(64, HMPC_SWING_WAVES) swing_kernel(SolveArgs a
     });
     const double objv = half_sum(objl);
     wsync();
-#ifdef HMPC_SWING_DEBUG
-    wsync();
-    xo[hl] = dbg0;
-    xo[32 + hl] = dbg1;
-    xo[64 + hl] = dbg2;
-    xo[96 + hl] = dbg3;
-    wsync();
-#endif
 #ifdef HMPC_STAMPS
     SW_STAMP(8);
     if (hl < 16) xo[hl] = __longlong_as_double(stamp_[hl]);   // (lane-uniform stamps)

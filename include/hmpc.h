@@ -243,7 +243,11 @@ int hmpc_set_precision(hmpc_ctx* ctx, int precision);
 /* Number of fp64 corrections HMPC_PREC_F32_REFINED runs (0..16, default 5:
    each contracts the error by ~cond x eps32, measured max|du| 1.7e-3 / 7.4e-5 /
    3.1e-6 / 1.3e-7 / 6.4e-9 after 2 / 3 / 4 / 5 / 6 on configs[4]; each costs an
-   fp64 rollout + adjoint and two fp32 sweeps per instance). */
+   fp64 rollout + adjoint and two fp32 sweeps per instance).  An instance is
+   accepted only when its last correction is below 4e-6 (converged), so with
+   fewer than about 4 corrections -- 0 included -- nearly every instance fails
+   that check and is re-solved by the fp64 overflow pass: the results stay
+   exact, the cost is that of the fp64 pass for the whole batch. */
 int hmpc_set_refinement(hmpc_ctx* ctx, int corrections);
 
 /* Instance order of later solves (results do not depend on it):

@@ -31,7 +31,7 @@ for cfg in $CFGS; do
   run() {
     local name=$1; shift
     timeout -s KILL 120 rocprofv3 --pmc "$@" -f csv -d $O/pmc_$name -o run -- \
-      python3 $R/bench.py $A --steps 3 --warmup 1 --cpu-seconds 0 > $O/pmc_$name.log 2>&1
+      python3 $R/bench.py $A --steps 3 --warmup 1 --prewarm-ms 0 --cpu-seconds 0 > $O/pmc_$name.log 2>&1
   }
   run sq1 SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_WAIT_ANY || { echo "$cfg sq1 failed"; exit 1; }
   run fetch FETCH_SIZE || { echo "$cfg fetch failed"; exit 1; }

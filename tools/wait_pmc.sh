@@ -15,7 +15,7 @@ cd /tmp && export TMPDIR=/tmp
 run() {
   local name=$1; shift
   timeout -s KILL 150 rocprofv3 --pmc "$@" -f csv -d $O/pmc_$name -o run -- \
-    python3 $R/bench.py "${BARGS[@]}" --steps 3 --warmup 1 --cpu-seconds 0 > $O/pmc_$name.log 2>&1
+    python3 $R/bench.py "${BARGS[@]}" --steps 3 --warmup 1 --prewarm-ms 0 --cpu-seconds 0 > $O/pmc_$name.log 2>&1
 }
 BARGS=("$@")
 run vlat VmemLatency || { echo "$NAME vlat failed"; exit 1; }
