@@ -96,31 +96,9 @@ constexpr int PS_OFF = 0, P2_OFF = 144, TS_OFF = 288, FS_OFF = 360, GS_OFF = 432
 // lower; G_k^-1 = Dinv_k' Dinv_k) of every stage -- written by the
 // factorisation, read by every sweep
 __host__ __device__ inline int64_t ric_kws_doubles(int N) { return ((93 * (int64_t)N) + 15) & ~(int64_t)15; }
-// the factorisation kernel's per-instance output (ric_kinst_stride): one
-// record [K_k (72) | BW_k (18)] per stage (kRecS doubles, 16-B aligned: the
-// solve kernel's sweeps stream whole records into LDS by LDS-DMA), then Dinv_k
-// of every stage (21 each), then a flag (nonzero: a non-positive pivot)
-constexpr int kRecS = 90;
-__host__ __device__ inline int64_t ric_kinst_doubles(int N) { return (((kRecS + 21) * (int64_t)N + 1) + 15) & ~(int64_t)15; }
-
-// LDS-DMA (gfx950 global_load_lds_dwordx4): 16 B per active lane from the
-// lane's source address to lds_base + 16 * lane.  M0 carries the LDS base and
-// is saved / restored inside the statement (the compiler reserves it).  The
-// load is on the VM counter and invisible to the compiler's waitcnt
-// bookkeeping: its consumers wait with vm_wait<n>() (n = the VM operations
-// issued after it; the counter retires in issue order, so a count that also
-// covers compiler-issued operations only waits longer).
-__device__ __forceinline__ void lds_dma16(const void* src, unsigned lds_base) {
-  unsigned keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep)
-               : "v"(src), "s"(lds_base)
-               : "memory");
-}
-template <int C>
-__device__ __forceinline__ void vm_wait() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(C) : "memory");
-}
+// the factorisation kernel's per-instance output (ric_kinst_stride): K / Dinv
+// of every stage, then a flag (nonzero: a non-positive pivot)
+__host__ __device__ inline int64_t ric_kinst_doubles(int N) { return ((93 * (int64_t)N + 1) + 15) & ~(int64_t)15; }
 
 __device__ __forceinline__ int loff(int r) { return (r * (r + 1)) >> 1; }
 
@@ -226,21 +204,8 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
   double* zv = sm + L.ZV;
   double* nb = sm + L.NB;
   double* mu_ = sm + L.MU;
-  // K_k (global): the fused kernel's workgroup slot (stride 72), or the
-  // factorisation kernel's per-instance records [K_k | BW_k] (stride kRecS)
-  constexpr bool kRec = PART != 0;
-  constexpr int KS = kRec ? kRecS : 72;
-  double* km = kw;
-  double* gi = kw + KS * N;   // Dinv_k, G_k^-1 = Dinv'Dinv (global workspace, packed lower 21)
-  // the one-wave solve kernel (PART 2): the sweeps stream the stage records
-  // [K_k | BW_k] into a ring of kRS LDS slots over BW (dead during the
-  // sweeps; reloaded from the records for the outputs), kRS - 2 stages ahead
-  // of the register ring -- the K loads no longer wait on L2 / MALL latency
-  // inside the sweep's chain
-  constexpr bool kDma = PART == 2 && RING == 3 && ENT == 1;
-  constexpr int kRS = NC > 0 ? (NC / 5 < 8 ? NC / 5 : 8) : 5;   // slots (18 N >= kRecS kRS for N >= 25)
-  static_assert(!kDma || kRS >= 4, "ring depth");
-  [[maybe_unused]] const double* const flagp = kw + (KS + 21) * N;
+  double* km = kw;            // K_k (global workspace)
+  double* gi = kw + 72 * N;   // Dinv_k, G_k^-1 = Dinv'Dinv (global workspace, packed lower 21)
   double* ua = sm + L.UA;
   int* act = reinterpret_cast<int*>(sm + L.ACT);
   double* cbv = sm + L.CB;
@@ -282,12 +247,6 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
     stage_dynamics_vals<VAR, double>(k, row[5], p, pfk, a.Jinv, a.rh, dt, cs, bw);
   }
   wsync();
-  if constexpr (PART == 1) {   // BW_k into the stage records (the solve kernel's sweeps stream them)
-    for (int i = lane; i < 18 * N; i += RT) {
-      const int k = i / 18;
-      km[KS * k + 72 + (i - 18 * k)] = bw[i];
-    }
-  }
 
   RS_ACC(0, t_p0);
   RS_T(t_p1);
@@ -349,7 +308,7 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
   // the overhang, both in one unrolled body (their LDS latencies overlap).
   int status = ST_SOLVED;
   if constexpr (PART == 2) {   // factorised by the factorisation kernel
-    if (*flagp != 0.0) status = ST_NUMERICAL;
+    if (kw[93 * N] != 0.0) status = ST_NUMERICAL;
   } else {
     double* Pc = un + PS_OFF;   // P_{k+1}, 12 x 12 full
     double* Pn = un + P2_OFF;   // P_k
@@ -518,7 +477,7 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
           double s = 0.0;
 #pragma unroll
           for (int m = c; m < 6; ++m) s = fma(Di[loff(m) + c], y[m], s);
-          km[KS * k + 12 * c + j] = s;
+          km[72 * k + 12 * c + j] = s;
           Kl[6 * j + c] = s;
         }
       }
@@ -567,7 +526,7 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
     if (nbad != 0.0) status = ST_NUMERICAL;
   }
   if constexpr (PART == 1) {   // the factorisation kernel: the pivot flag, then done
-    if (lane == 0) kw[(KS + 21) * N] = status == ST_SOLVED ? 0.0 : 1.0;
+    if (lane == 0) kw[93 * N] = status == ST_SOLVED ? 0.0 : 1.0;
     return;
   }
   gsync();   // K, Dinv (global) visible to every lane of the workgroup
@@ -655,7 +614,7 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
       d.b2 = bw[18 * j + 12 + c6];
       if constexpr (MR) d.n = colb[6 * j + c6];
       else d.n = nb[6 * j + c6];
-      const double* kcol = km + KS * j + (lr < 12 ? lr : 0);
+      const double* kcol = km + 72 * j + (lr < 12 ? lr : 0);
   #pragma unroll
       for (int c = 0; c < 6; ++c) d.kc[c] = kcol[12 * c];
       asm volatile("" ::: "memory");   // issue here, two steps ahead of the use
@@ -665,7 +624,7 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
       d.sp = cs[2 * k + 1];
       if constexpr (MR) d.w = colb[6 * k + c6];
       else d.w = mu_[6 * k + c6];
-      const double* krow = km + KS * k + 12 * c6;
+      const double* krow = km + 72 * k + 12 * c6;
   #pragma unroll
       for (int c = 0; c < 12; ++c) d.kr[c] = krow[c];
       const int rr = (lr >= 9 && lr < 12) ? lr - 9 : 0;
@@ -673,39 +632,6 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
       for (int c = 0; c < 6; ++c) d.br[c] = bw[18 * k + 6 * rr + c];
       asm volatile("" ::: "memory");   // issue here, two steps ahead of the use
     };
-    // kDma: the same fields from an LDS ring slot holding the record
-    // [K_k | BW_k]; lds_dma16 by lanes < kRecS / 2 fills a slot in one
-    // instruction
-    constexpr bool DMA = kDma && MR;
-    [[maybe_unused]] const int rl = lr < 12 ? lr : 0;
-    [[maybe_unused]] auto slot_b = [&](const double* sl, int j, BwdL& d) __attribute__((always_inline)) {
-      d.cp = cs[2 * j];
-      d.sp = cs[2 * j + 1];
-      d.st = cc[j];
-      d.b0 = sl[72 + c6];
-      d.b1 = sl[72 + 6 + c6];
-      d.b2 = sl[72 + 12 + c6];
-      d.n = colb[6 * j + c6];
-  #pragma unroll
-      for (int c = 0; c < 6; ++c) d.kc[c] = sl[12 * c + rl];
-      asm volatile("" ::: "memory");
-    };
-    [[maybe_unused]] auto slot_f = [&](const double* sl, int k, FwdL& d) __attribute__((always_inline)) {
-      d.cp = cs[2 * k];
-      d.sp = cs[2 * k + 1];
-      d.w = colb[6 * k + c6];
-  #pragma unroll
-      for (int c = 0; c < 12; ++c) d.kr[c] = sl[12 * c6 + c];
-      const int rr = (lr >= 9 && lr < 12) ? lr - 9 : 0;
-  #pragma unroll
-      for (int c = 0; c < 6; ++c) d.br[c] = sl[72 + 6 * rr + c];
-      asm volatile("" ::: "memory");
-    };
-    [[maybe_unused]] const unsigned ring0 = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(uintptr_t)bw);
-    [[maybe_unused]] auto dma = [&](int stage, int slot) __attribute__((always_inline)) {
-      if (lane < kRecS / 2) lds_dma16(km + KS * stage + 2 * lane, ring0 + (unsigned)(8 * kRecS) * (unsigned)slot);
-    };
-    auto next = [](int sl) { return sl + 1 == kRS ? 0 : sl + 1; };
     // ---- backward sweep
     {
       double li = 0.0;                                  // lam_{j+1}[lane]
@@ -762,41 +688,7 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
       // (loads are unconditional -- out-of-range steps reload stage 0 -- so
       // that the vmcnt/lgkmcnt waits stay counted, not drained)
       static_assert(RING == 2 || RING == 3, "ring depth");
-      if constexpr (DMA) {
-        // stage t lives in slot (jt - t) mod kRS; the record of stage j - kRS
-        // is issued once bstep(j) has consumed slot j's registers, so a
-        // record lands kRS - 2 steps before the register ring reads it
-        BwdL R0, R1, R2;
-#pragma unroll
-        for (int i = 0; i < kRS; ++i) dma(jt - i >= 0 ? jt - i : 0, i);
-        vm_wait<kRS - 1>();
-        slot_b(bw, jt, R0);
-        vm_wait<kRS - 2>();
-        slot_b(bw + kRecS, jt >= 1 ? jt - 1 : 0, R1);
-        int rs = 2, ws = 0;
-        for (int j = jt; j >= 0; j -= 3) {
-          vm_wait<kRS - 3>();
-          slot_b(bw + kRecS * rs, j >= 2 ? j - 2 : 0, R2);
-          rs = next(rs);
-          bstep(j, R0);
-          if (j < 1) break;
-          dma(j - kRS >= 0 ? j - kRS : 0, ws);
-          ws = next(ws);
-          vm_wait<kRS - 3>();
-          slot_b(bw + kRecS * rs, j >= 3 ? j - 3 : 0, R0);
-          rs = next(rs);
-          bstep(j - 1, R1);
-          if (j < 2) break;
-          dma(j - 1 - kRS >= 0 ? j - 1 - kRS : 0, ws);
-          ws = next(ws);
-          vm_wait<kRS - 3>();
-          slot_b(bw + kRecS * rs, j >= 4 ? j - 4 : 0, R1);
-          rs = next(rs);
-          bstep(j - 2, R2);
-          dma(j - 2 - kRS >= 0 ? j - 2 - kRS : 0, ws);
-          ws = next(ws);
-        }
-      } else if constexpr (RING == 3) {
+      if constexpr (RING == 3) {
         BwdL R0, R1, R2;
         load_b(jt, R0);
         load_b(jt >= 1 ? jt - 1 : 0, R1);
@@ -919,40 +811,7 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
         }
         xi = lr < 12 ? (b0 + b1) + b2 : 0.0;
       };
-      if constexpr (DMA) {
-        // stage t in slot t mod kRS (as the backward sweep)
-        FwdL R0, R1, R2;
-        auto cl = [&](int t) { return t < N ? t : N - 1; };
-#pragma unroll
-        for (int i = 0; i < kRS; ++i) dma(cl(i), i);
-        vm_wait<kRS - 1>();
-        slot_f(bw, 0, R0);
-        vm_wait<kRS - 2>();
-        slot_f(bw + kRecS, cl(1), R1);
-        int rs = 2, ws = 0;
-        for (int k = 0; k < N; k += 3) {
-          vm_wait<kRS - 3>();
-          slot_f(bw + kRecS * rs, cl(k + 2), R2);
-          rs = next(rs);
-          fstep(k, R0);
-          if (k + 1 >= N) break;
-          dma(cl(k + kRS), ws);
-          ws = next(ws);
-          vm_wait<kRS - 3>();
-          slot_f(bw + kRecS * rs, cl(k + 3), R0);
-          rs = next(rs);
-          fstep(k + 1, R1);
-          if (k + 2 >= N) break;
-          dma(cl(k + 1 + kRS), ws);
-          ws = next(ws);
-          vm_wait<kRS - 3>();
-          slot_f(bw + kRecS * rs, cl(k + 4), R1);
-          rs = next(rs);
-          fstep(k + 2, R2);
-          dma(cl(k + 2 + kRS), ws);
-          ws = next(ws);
-        }
-      } else if constexpr (RING == 3) {
+      if constexpr (RING == 3) {
         FwdL R0, R1, R2;
         load_f(0, R0);
         load_f(N >= 2 ? 1 : 0, R1);
@@ -1521,12 +1380,6 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
       a.ovf_list[slot] = (int32_t)b;
     }
     return;
-  }
-  if constexpr (kDma) {   // BW again (the sweeps' ring overwrote it) from the stage records
-    for (int i = lane; i < 18 * N; i += RT) {
-      const int k = i / 18;
-      bw[i] = km[KS * k + 72 + (i - 18 * k)];
-    }
   }
   // x_ref into the union again (over the dead R), x* staged over SV..
   for (int i = lane; i < 12 * N; i += RT) {
