@@ -35,7 +35,7 @@ for step in "$@"; do
     bench)
       timeout -k 10 400 python bench.py $(sp $a2) > $OUT/bench_$a1.json 2> $OUT/bench_$a1.err; rc=$?
       stop $rc; [ $rc -eq 0 ] || { echo "bench $a1 failed"; tail -5 $OUT/bench_$a1.err; exit 1; }
-      python -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], round(d['value']/1e6,3), 'M/s', d['ms_per_step'], 'ms', d.get('parity_sample',{}).get('max_abs_du_vs_port'))" \
+      python -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], round(d['value']/1e6,3), 'M/s', d['ms_per_step'], 'ms', (d.get('parity_sample') or {}).get('max_abs_du_vs_port'))" \
         $OUT/bench_$a1.json $a1 ;;
     trace)
       (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $OUT/trace_$a1 -o run -- \
