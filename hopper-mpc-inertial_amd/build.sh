@@ -57,12 +57,18 @@ for n in $HORIZONS; do
   fi
   while [ "$(jobs -rp | wc -l)" -ge "$JOBS" ]; do sleep 1; done
 done
+# the fp32 builds' all-swing class (F32_SWING=0 disables): the fp64 swing
+# kernel (two instances per wave, the torque-only QP), so fp32 and fp64 run
+# the same three classes
+F32_SWING=${F32_SWING-1}
 for n in $F32_HORIZONS; do
   # fp32: 3 waves / SIMD fit (<= 168 VGPRs, 9.9 KB LDS) without spilling;
   # split like fp64, the compacted class at 4 waves / SIMD
   F32C=$(cmp_flags $n "$F32_CMP")
+  F32SW=""
+  if [ "$F32_SWING" = 1 ] && [ -n "$(swing_flags $n)" ] && [ -n "$F32C" ]; then F32SW="-DHMPC_SWING=1 $(swing_flags $n)"; fi
   $HIPCC $FLAGS -DHMPC_INST_N=$n -DHMPC_REAL=float -DHMPC_LAUNCH_SUFFIX=_f32 "-DHMPC_WAVES_PER_EU(W)=$F32_WAVES" \
-    $F32C -c ${KSRC:-csrc/hmpc_kernels.hip} -o $BDIR/hmpc_kernels_n${n}_f32.o "$@" &
+    $F32C $F32SW -c ${KSRC:-csrc/hmpc_kernels.hip} -o $BDIR/hmpc_kernels_n${n}_f32.o "$@" &
   pids+=($!)
   if [ -n "$F32C" ]; then
     $HIPCC $FLAGS -DHMPC_INST_N=$n -DHMPC_REAL=float -DHMPC_LAUNCH_SUFFIX=_f32 "-DHMPC_WAVES_PER_EU(W)=$F32_WAVES" \
@@ -73,7 +79,7 @@ for n in $F32_HORIZONS; do
   # fp32 + fp64 refinement (HMPC_PREC_F32_REFINED), split like the others:
   # every class at 2 waves / SIMD (no scratch spill)
   $HIPCC $FLAGS -DHMPC_INST_N=$n -DHMPC_REAL=float -DHMPC_F32_REFINE=1 -DHMPC_LAUNCH_SUFFIX=_f32r \
-    "-DHMPC_WAVES_PER_EU(W)=2" $F32C -c csrc/hmpc_kernels.hip -o $BDIR/hmpc_kernels_n${n}_f32r.o "$@" &
+    "-DHMPC_WAVES_PER_EU(W)=2" $F32C $F32SW -c csrc/hmpc_kernels.hip -o $BDIR/hmpc_kernels_n${n}_f32r.o "$@" &
   pids+=($!)
   if [ -n "$F32C" ]; then
     $HIPCC $FLAGS -DHMPC_INST_N=$n -DHMPC_REAL=float -DHMPC_F32_REFINE=1 -DHMPC_LAUNCH_SUFFIX=_f32r \

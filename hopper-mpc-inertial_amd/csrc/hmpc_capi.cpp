@@ -45,7 +45,8 @@ struct hmpc_ctx {
   // the counters need a zeroing before the next solve (fresh buffer, or a
   // solve whose overflow pass -- which zeroes them at its end -- did not run)
   bool ovf_dirty = true;
-  bool ovf_total_failed = false;   // the diagnostic counter could not be allocated
+  bool ovf_total_failed = false;
+  bool ovf2_zeroed = false;   // the second overflow header (run_solve) is zero   // the diagnostic counter could not be allocated
   double* rws = nullptr;
   // dense split launch: the three class lists [3][split_cap], or (longest-first
   // order) up to N + 1 stance-count buckets of split_cap entries; the Riccati
@@ -112,6 +113,7 @@ hmpc::SolveArgs make_args(hmpc_ctx* c, int64_t B, const double* x_in, const doub
   a.ws = nullptr; a.ws_stride = 0; a.ws_groups = 0;
   a.ovf_count = nullptr; a.ovf_list = nullptr; a.rws = nullptr; a.rws_stride = 0;
   a.ovf_total = nullptr;
+  a.ovf_hdr1 = nullptr;
   a.work = nullptr; a.kws = nullptr; a.kws_stride = 0; a.ric_groups = 0;
   a.kinst = nullptr; a.kinst_stride = 0;
   a.split_count = nullptr; a.split_list = nullptr; a.list = nullptr; a.list_count = nullptr;
@@ -249,10 +251,13 @@ int prepare_ric(hmpc_ctx* c, int64_t B, hmpc::SolveArgs& a) {
     if (c->ovf) (void)hipFree(c->ovf);
     c->ovf = nullptr;
     c->ovf_cap = 0;
-    hipError_t e = hipMalloc(&c->ovf, sizeof(int32_t) * (size_t)(B + kOvfHeader));
+    // [header | list of B] twice: the second pair serves the generic pass
+    // behind HMPC_PREC_F32_REFINED's fp64 dense fallback pass (run_solve)
+    hipError_t e = hipMalloc(&c->ovf, sizeof(int32_t) * 2 * (size_t)(B + kOvfHeader));
     if (e != hipSuccess) { c->err = "overflow list hipMalloc"; return HMPC_ERR_NOMEM; }
     c->ovf_cap = B;
     c->ovf_dirty = true;
+    c->ovf2_zeroed = false;
   }
   a.ovf_count = c->ovf;
   a.work = c->ovf + 1;
@@ -339,8 +344,16 @@ int prepare_ric(hmpc_ctx* c, int64_t B, hmpc::SolveArgs& a) {
   return HMPC_OK;
 }
 
+// The second overflow header and list (run_solve, HMPC_PREC_F32_REFINED)
+int32_t* ovf_hdr2(hmpc_ctx* c) { return c->ovf + kOvfHeader + c->ovf_cap; }
+
 // One solve pass over the batch: the main kernel, then (dense / Riccati
 // kernels) the overflow pass over the instances it handed on.  Stream-ordered.
+// HMPC_PREC_F32_REFINED hands on the instances its fp64 check rejected
+// (0.6 % of configs[4]): they are re-solved first by the fp64 dense kernel
+// over that list (its full class: the dense kernel's speed), and only what
+// outgrows that kernel's capacity goes on to the generic capacity-6N pass,
+// through the second header and list.
 int run_solve(hmpc_ctx* c, hmpc::SolveArgs a, hipStream_t s) {
   int rc = prepare_ws(c, a.B, a);
   if (rc != HMPC_OK) return rc;
@@ -351,16 +364,46 @@ int run_solve(hmpc_ctx* c, hmpc::SolveArgs a, hipStream_t s) {
   // every main pass that has one, zeroes them at its end (stream order: the
   // next solve's kernels see them zero).  The CasADi kernel has no overflow
   // pass.
+  const bool fb = a.ovf_count && hmpc::pick_kernel(c->variant, c->N, c->precision) == hmpc::Kernel::DenseF32R;
   if (a.work && (!a.ovf_count || c->ovf_dirty)) {
     hipError_t e = hipMemsetAsync(a.work - 1, 0, (a.ovf_count ? kOvfHeader : 3) * sizeof(int32_t), s);
     if (e != hipSuccess) return fail_hip(c, e, "hipMemsetAsync(overflow count)");
+  }
+  if (fb && (!c->ovf2_zeroed || c->ovf_dirty)) {   // (the generic pass zeroes it at its end)
+    hipError_t e = hipMemsetAsync(ovf_hdr2(c), 0, kOvfHeader * sizeof(int32_t), s);
+    if (e != hipSuccess) return fail_hip(c, e, "hipMemsetAsync(second overflow count)");
+    c->ovf2_zeroed = true;
   }
   c->ovf_dirty = true;   // until the overflow pass is launched
   if (!hmpc::launch_solve(c->variant, c->N, a, s)) {
     c->err = "no kernel for this (variant, N, precision)";
     return HMPC_ERR_UNSUPPORTED;
   }
-  if (a.ovf_count && !hmpc::launch_solve_ric_overflow(c->variant, c->N, a, kOvfGroups, s)) {
+  if (fb) {
+    hmpc::SolveArgs f = a;   // the fp64 dense kernel over the main pass's overflow list
+    f.precision = HMPC_PREC_F64;
+    f.list = a.ovf_list;
+    f.list_count = a.ovf_count;
+    f.lpt = 0;
+    f.lpt_lo = 0;
+    f.lpt_hi = -1;
+    f.split_count = nullptr;
+    f.split_list = nullptr;
+    f.ovf_count = ovf_hdr2(c);
+    f.ovf_list = ovf_hdr2(c) + kOvfHeader;
+    if (!hmpc::launch_solve_fp64_list(c->variant, c->N, f, s)) {
+      c->err = "fp64 fallback pass launch";
+      return HMPC_ERR_UNSUPPORTED;
+    }
+    hmpc::SolveArgs o = a;   // the generic pass over what that kernel handed on
+    o.ovf_count = f.ovf_count;
+    o.ovf_list = f.ovf_list;
+    o.ovf_hdr1 = a.ovf_count;
+    if (!hmpc::launch_solve_ric_overflow(c->variant, c->N, o, kOvfGroups, s)) {
+      c->err = "overflow pass launch";
+      return HMPC_ERR_UNSUPPORTED;
+    }
+  } else if (a.ovf_count && !hmpc::launch_solve_ric_overflow(c->variant, c->N, a, kOvfGroups, s)) {
     c->err = "overflow pass launch";
     return HMPC_ERR_UNSUPPORTED;
   }

@@ -22,6 +22,7 @@ namespace hmpc {
 
 #define HMPC_DECL(n)                                                       \
   bool launch_solve_n##n(int variant, const SolveArgs& a, hipStream_t s); \
+  bool launch_list_n##n(int variant, const SolveArgs& a, hipStream_t s);  \
   int qmax_solve_n##n();                                                  \
   int split_nv_n##n();                                                    \
   const char* name_solve_n##n(int variant);
@@ -94,6 +95,15 @@ Kernel pick_kernel(int variant, int N, int precision) {
     default:
       return Kernel::None;
   }
+}
+
+bool launch_solve_fp64_list(int variant, int N, const SolveArgs& a, hipStream_t s) {
+  if (variant != 2 && variant != 3) return false;
+#define HMPC_CASE(n) \
+  if (N == n) return launch_list_n##n(variant, a, s);
+  HMPC_HORIZON_LIST(HMPC_CASE)
+#undef HMPC_CASE
+  return false;
 }
 
 bool launch_solve(int variant, int N, const SolveArgs& a, hipStream_t s) {

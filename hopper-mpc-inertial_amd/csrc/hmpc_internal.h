@@ -58,6 +58,12 @@ struct SolveArgs {
   // running total of the instances the overflow pass re-solved on this
   // context (hmpc_overflow_total), or nullptr
   unsigned long long* ovf_total;
+  // a second overflow header (HMPC_PREC_F32_REFINED): the instances of
+  // ovf_list were first re-solved by the fp64 dense kernel (launch_solve_fp64_list),
+  // whose own overflows went to this pass's list; the pass zeroes that first
+  // header (count, counters, split counts) too and counts its instances in
+  // ovf_total.  nullptr: one header.
+  int32_t* ovf_hdr1;
   double* rws;
   int64_t rws_stride;
   // Riccati kernel (persistent): instance counter (zeroed before the launch),
@@ -124,6 +130,10 @@ int64_t ric_kinst_stride(int N, int64_t B);
 // horizon N (0: plain index order); their lists take buckets x B ints
 int ric_lpt_buckets(int N);
 bool launch_solve_ric(int variant, int N, const SolveArgs& a, hipStream_t stream);
+// the fp64 dense kernel of horizon N (its full class: any free-variable
+// count) over a.list / *a.list_count, one workgroup per entry, grid a.B; false
+// when no dense fp64 object serves N.  HMPC_PREC_F32_REFINED's fallback pass.
+bool launch_solve_fp64_list(int variant, int N, const SolveArgs& a, hipStream_t s);
 // the overflow pass over a.ovf_list (count on the device), <= groups workgroups
 bool launch_solve_ric_overflow(int variant, int N, const SolveArgs& a, int groups, hipStream_t s);
 

@@ -58,6 +58,7 @@
 
 #ifndef HMPC_REAL
 #define HMPC_REAL double
+#define HMPC_REAL_FP64 1   // (the default fp64 objects)
 #endif
 
 namespace hmpc {
@@ -2235,6 +2236,26 @@ bool HMPC_CAT(HMPC_CAT(launch_solve_n, HMPC_INST_N), HMPC_LAUNCH_SUFFIX)(int var
   else hipLaunchKernelGGL((solve_kernel<2, N, real>), dim3((unsigned)a.B), dim3(NT), 0, s, af);
   return true;
 }
+
+#ifdef HMPC_REAL_FP64
+// the fp64 objects only (HMPC_LAUNCH_SUFFIX empty): the full-class kernel
+// (any free-variable count) over a caller's list -- HMPC_PREC_F32_REFINED's
+// fallback pass re-solves the instances its fp64 check rejected here, at the
+// dense kernel's speed, instead of in the generic capacity-6N pass
+bool HMPC_CAT(HMPC_CAT(launch_list_n, HMPC_INST_N), HMPC_LAUNCH_SUFFIX)(int variant, const SolveArgs& a,
+                                                                    hipStream_t s) {
+  constexpr int N = HMPC_INST_N;
+  if (a.B <= 0) return true;
+  if (!a.list || !a.list_count) return false;
+  if (variant == 3) hipLaunchKernelGGL((solve_kernel<3, N, real>), dim3((unsigned)a.B), dim3(Lay<N>::NT), 0, s, a);
+#ifdef HMPC_FULL2F_NV
+  else HMPC_FULL2F_LAUNCH(a, s);
+#else
+  else hipLaunchKernelGGL((solve_kernel<2, N, real>), dim3((unsigned)a.B), dim3(Lay<N>::NT), 0, s, a);
+#endif
+  return true;
+}
+#endif
 
 // this object's active-set capacity and kernel names (hmpc_active_capacity,
 // hmpc_kernel_name: read from here, not restated in the C API)

@@ -125,9 +125,14 @@ __device__ __forceinline__ void gsync() { __syncthreads(); }
 #ifdef HMPC_STAMPS
 #define RS_T(v) const long long v = __builtin_amdgcn_s_memtime()
 #define RS_ACC(slot, v) (rst_[slot] += __builtin_amdgcn_s_memtime() - (v))
+// event counts (stamped builds): slots 11-14 time the factorisation's parts
+// where the kernel factorises, else they count s sweep pairs, MRHS cache
+// hits, z fallback sweeps and right-hand sides per sweep pair
+#define RS_CNT(slot, n) (rst_[slot] += (n))
 #else
 #define RS_T(v) ((void)0)
 #define RS_ACC(slot, v) ((void)0)
+#define RS_CNT(slot, n) ((void)0)
 #endif
 
 // inclusive prefix sum over the wave (lane order): Hillis-Steele inside each
@@ -1014,6 +1019,7 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
       // other stages (MRHS)
       const uint64_t hit = __ballot(lane < kNSC && cid == p);
       if (hit) {
+        if constexpr (PART == 2) RS_CNT(12, 1);
         const double* col = gcache + (int64_t)__builtin_ctzll(hit) * NV;
         for (int i = lane; i < NV; i += RT) sv[i] = col[i];
         wsync();
@@ -1048,6 +1054,7 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
           }
         }
         const int row = lane >> 4;
+        if constexpr (PART == 2) { RS_CNT(11, 1); RS_CNT(14, nr); }
         if constexpr (kMRL) {
           // the four columns in LDS vectors that are dead during this sweep
           // pair: SV (row 0, so s lands in place), ZV, MU and the union's
@@ -1258,6 +1265,7 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
             const int ai = 64 * e + lane;
             if (ai < q) tz = max(tz, stage_top(act[ai]));
           }
+          if constexpr (PART == 2) RS_CNT(13, 1);
           hinv(zv, wave_imax63(tz));
           zn = vdot(nb, zv);
         }
@@ -1506,11 +1514,20 @@ template <int VAR>
 __global__ void __launch_bounds__(RT) ric_overflow_kernel(SolveArgs a, int N) {
   extern __shared__ __attribute__((aligned(16))) double ric_sm[];
   const int n = *a.ovf_count;
+  // the header holding the split counts: the first one when the fp64 dense
+  // fallback pass ran in between (a.ovf_hdr1, HMPC_PREC_F32_REFINED), whose
+  // instances the running total counts (this pass re-solves a subset of them)
+  int32_t* const h1 = a.ovf_hdr1 ? a.ovf_hdr1 : a.ovf_count;
   if (n == 0) {
     // nothing to re-solve (the usual case): no block depends on the counters
     // any more, so block 0 zeroes them at once, without the done counter's
     // one serialised atomic per workgroup
-    if (blockIdx.x == 0 && (int)threadIdx.x < 3 + a.split_nbkt) a.ovf_count[threadIdx.x] = 0;
+    if (blockIdx.x == 0) {
+      // (thread 0 reads the first count before it zeroes it itself)
+      if (a.ovf_hdr1 && threadIdx.x == 0 && a.ovf_total) atomicAdd(a.ovf_total, (unsigned long long)h1[0]);
+      if ((int)threadIdx.x < 3) a.ovf_count[threadIdx.x] = 0;
+      if ((int)threadIdx.x < 3 + a.split_nbkt) h1[threadIdx.x] = 0;
+    }
     return;
   }
   double* Rm = a.rws + (int64_t)blockIdx.x * a.rws_stride;
@@ -1528,11 +1545,13 @@ __global__ void __launch_bounds__(RT) ric_overflow_kernel(SolveArgs a, int N) {
   if (threadIdx.x == 0) {
     __threadfence();
     if (atomicAdd(a.ovf_count + 2, 1) == (int)gridDim.x - 1) {
-      if (a.ovf_total) atomicAdd(a.ovf_total, (unsigned long long)n);
+      if (a.ovf_total) atomicAdd(a.ovf_total, (unsigned long long)(a.ovf_hdr1 ? h1[0] : n));
       atomicExch(a.ovf_count, 0);
       atomicExch(a.ovf_count + 1, 0);
       atomicExch(a.ovf_count + 2, 0);
-      for (int i = 0; i < a.split_nbkt; ++i) atomicExch(a.ovf_count + 3 + i, 0);   // the dense split's counts
+      if (a.ovf_hdr1)
+        for (int i = 0; i < 3; ++i) atomicExch(h1 + i, 0);
+      for (int i = 0; i < a.split_nbkt; ++i) atomicExch(h1 + 3 + i, 0);   // the dense split's counts
     }
   }
 }

@@ -70,10 +70,12 @@ def test_kernel_names(hm):
     assert make(hm, 10, 'f64_riccati').kernel_name == 'hmpc::ric_kernel<3, 2, 0, 0, 0>'
     assert make(hm, 20, 'f64_dense').kernel_name == 'hmpc::solve_kernel<3, 20, double, 0, 0>'
     assert make(hm, 10, 'f64_generic').kernel_name == 'hmpc::wide_kernel<3, double>'
-    assert make(hm, 10, 'f32').kernel_name == ('hmpc::solve_kernel<3, 10, float, 48, 13> + '
-                                               'hmpc::solve_kernel<3, 10, float, 0, 0>')   # fp32 split
-    assert make(hm, 10, 'f32_refined').kernel_name == ('hmpc::solve_kernel<3, 10, float, 48, 13> + '
-                                                       'hmpc::solve_kernel<3, 10, float, 0, 0>')   # split (round 5)
+    # fp32 split: the fp64 all-swing class + compacted + full (round 6)
+    assert make(hm, 10, 'f32').kernel_name == ('hmpc::swing_kernel<10, 13> + hmpc::solve_kernel<3, 10, float, 48, 13> + '
+                                               'hmpc::solve_kernel<3, 10, float, 0, 0>')
+    assert make(hm, 10, 'f32_refined').kernel_name == ('hmpc::swing_kernel<10, 13> + '
+                                                       'hmpc::solve_kernel<3, 10, float, 48, 13> + '
+                                                       'hmpc::solve_kernel<3, 10, float, 0, 0>')
     assert make(hm, 20, 'f32').kernel_name == 'hmpc::wide_kernel<3, float>'   # no fp32 dense build
     assert make(hm, 10, 'f32_generic').kernel_name == 'hmpc::wide_kernel<3, float>'
 

@@ -55,7 +55,8 @@ def test_fp32_dense_bounded(hm, variant, curve, musweep):
     # (2f: the 5N-wide kernel)
     full = f'hmpc::solve_kernel<{v}, 10, float, 0, 0>' if v == '3' else 'hmpc::solve_kernel<2, 10, float, 50, 20>'
     if not os.environ.get('HMPC_LIB'):   # (A/B builds may differ)
-        assert name == f'hmpc::solve_kernel<{v}, 10, float, 48, 13> + {full}', name
+        # (+ the all-swing class, fp64, round 6: off in this batch's longest-first order)
+        assert name == f'hmpc::swing_kernel<10, 13> + hmpc::solve_kernel<{v}, 10, float, 48, 13> + {full}', name
     ref = port.solve_batch(variant, N, inst['x_in'], inst['x_lin'], inst['x_ref'], inst['pf'], inst['C'],
                            mu=inst['mu'], nthreads=16)
     assert np.array_equal(g['status'], ref['status'])
@@ -113,7 +114,7 @@ def test_fp32_refined_meets_the_fp64_tolerance(hm, variant, curve, musweep):
     g, name = solve(hm, 'f32_refined', inst, N, variant, refine=5)
     v = variant[0]
     full = f'hmpc::solve_kernel<{v}, 10, float, 0, 0>' if v == '3' else 'hmpc::solve_kernel<2, 10, float, 50, 20>'
-    assert name == f'hmpc::solve_kernel<{v}, 10, float, 48, 13> + {full}', name   # split (round 5)
+    assert name == f'hmpc::swing_kernel<10, 13> + hmpc::solve_kernel<{v}, 10, float, 48, 13> + {full}', name
     ref = port.solve_batch(variant, N, inst['x_in'], inst['x_lin'], inst['x_ref'], inst['pf'], inst['C'],
                            mu=inst['mu'], nthreads=16)
     assert np.array_equal(g['status'], ref['status'])
@@ -167,3 +168,37 @@ def test_fp32_refined_unconverged_goes_to_fp64(hm):
     assert np.abs(g['u'][ok] - ref['u'][ok]).max() <= 1e-6
     assert fallbacks >= ok.sum()          # every solved instance went to the fp64 pass
     assert fallbacks5 < 0.05 * B, fallbacks5   # five corrections converge almost everywhere
+
+
+@pytest.mark.parametrize('precision', ['f32', 'f32_refined'])
+def test_fp32_builds_run_the_fp64_swing_class(hm, precision):
+    """Round 6: the fp32 builds split into the same three
+    classes as fp64, the all-swing windows (no stance stage: the torque-only
+    QP) solved by the fp64 swing kernel, two instances per wave.  In index
+    order that class runs at any batch size: its instances equal the port to
+    the fp64 tolerance, the others keep the fp32 (or refined) bound."""
+    import hmpc_plan
+    from oracle import port
+    N, B = 10, 2048
+    inst = hmpc_plan.sample_instances(B, N, curve=True, seed=95)
+    c = hmpc_plan.runner_constants()
+    cx = hm.Context('3f', N, t=c['t'], m=c['m'], g=c['g'], mu=1.0, Jinv=c['Jinv'], rh=c['rh'],
+                    precision=precision)
+    cx.set_order('index')
+    if precision == 'f32_refined':
+        cx.set_refinement(5)
+    g = cx.solve_host(inst['x_in'], inst['x_lin'], inst['x_ref'], inst['pf'], inst['C'], mu=inst['mu'])
+    cx.close()
+    ref = port.solve_batch('3f', N, inst['x_in'], inst['x_lin'], inst['x_ref'], inst['pf'], inst['C'],
+                           mu=inst['mu'], nthreads=16)
+    assert np.array_equal(g['status'], ref['status'])
+    ok = ref['status'] == 0
+    swing = (inst['C'] == 0).all(axis=1)
+    assert (swing & ok).sum() >= 200, swing.sum()
+    du = np.abs(g['u'] - ref['u']).max(axis=(1, 2))
+    assert du[swing & ok].max() <= 1e-6, du[swing & ok].max()
+    rel = np.abs(g['obj'] - ref['obj']) / np.abs(ref['obj'])
+    assert rel[swing & ok].max() <= 1e-9
+    assert np.abs(g['x'][swing & ok] - ref['x'][swing & ok]).max() <= 1e-6
+    bound = 2.0 if precision == 'f32' else 1e-6
+    assert du[ok].max() <= bound, du[ok].max()

@@ -14,6 +14,7 @@
 #   runner                      tools/runner_time.py, eager and graph replay
 #   stamps:TAG:LIB:ENV          tools/phase_stamps.py with HMPC_LIB=LIB and ENV
 #                               (NAME=VALUE pairs)
+#   ricstamps:TAG:LIB:ARGS      tools/ric_stamps.py ARGS with HMPC_LIB=LIB
 #   ab:TAG:ARGS:LIB,LIB         tools/ab.py interleaved A/B (3 rounds)
 #   profile:TAG                 tools/profile.sh TAG (all configurations)
 #   waits:TAG:CFG:ARGS          tools/wait_pmc.sh (latency decomposition)
@@ -50,6 +51,10 @@ for step in "$@"; do
       envs=$(sp $a3)
       env HMPC_LIB=hopper-mpc-inertial_amd/$a2 $envs timeout -k 10 180 python tools/phase_stamps.py \
         > $OUT/stamps_$a1.json 2> $OUT/stamps_$a1.err || { echo "stamps $a1 failed"; exit 1; } ;;
+    ricstamps)
+      HMPC_LIB=hopper-mpc-inertial_amd/$a2 timeout -k 10 200 python tools/ric_stamps.py $(sp $a3) \
+        > $OUT/ricstamps_$a1.json 2> $OUT/ricstamps_$a1.err || { echo "ricstamps $a1 failed"; tail -3 $OUT/ricstamps_$a1.err; exit 1; }
+      cat $OUT/ricstamps_$a1.json ;;
     ab)
       timeout -k 10 1000 python tools/ab.py --tag $a1 --rounds ${ROUNDS:-3} --args "$(sp $a2)" $(sp $a3) \
         > $OUT/ab_$a1.log 2>&1; rc=$?

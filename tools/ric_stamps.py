@@ -44,7 +44,11 @@ def main():
         out = ctx.solve_device(d['x_in'], d['x_lin'], d['x_ref'], d['pf'], d['C'], mu=d['mu'])
     torch.cuda.synchronize()
     st = out['x'].view(torch.int64).reshape(B, -1)[:, :len(NAMES)].cpu().numpy().astype(np.float64)
-    res = {n: float(st[:, i].mean()) for i, n in enumerate(NAMES)}
+    names = NAMES if N <= 24 else NAMES[:11] + ['count_s_sweep_pairs', 'count_mrhs_cache_hits',
+                                                 'count_z_fallback_sweeps', 'count_rhs_in_sweep_pairs']
+    res = {n: float(st[:, i].mean()) for i, n in enumerate(names)}
+    if N > 24:   # the factorisation kernel ran separately: slots 11-14 are event counts
+        res['count_z_fallback_sweeps_max'] = float(st[:, 13].max())
     res['iters_mean'] = float(out['iters'].float().mean())
     res['config'] = f'{var} N={N} B={B} {" ".join(flags)}'
     print(json.dumps(res))
