@@ -1180,14 +1180,21 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
           if (ai < q) cbv[ai] = rv[e];
         }
         rsync();
-        for (int j = lane; j < N; j += RT) {
-          double acc[6] = {0, 0, 0, 0, 0, 0};
-          add_coef(p, j, 1.0, acc);
-          for (int ai = 0; ai < q; ++ai) add_coef(act[ai], j, -cbv[ai], acc);
+        // n_z = n_p - N_A r is formed only for the sweep fallback below: the
+        // step's n_z'z equals n_p'z (N_A'z = c - R'R r = 0), the classic
+        // Goldfarb-Idnani denominator, so NB keeps n_p (round 6: the
+        // per-stage loop over every active row cost ~20 % of this phase at
+        // N = 60, where the fallback runs 0.006 times per instance)
+        auto nz_to_nb = [&]() __attribute__((always_inline)) {
+          for (int j = lane; j < N; j += RT) {
+            double acc[6] = {0, 0, 0, 0, 0, 0};
+            add_coef(p, j, 1.0, acc);
+            for (int ai = 0; ai < q; ++ai) add_coef(act[ai], j, -cbv[ai], acc);
 #pragma unroll
-          for (int c = 0; c < 6; ++c) nb[6 * j + c] = acc[c];
-        }
-        rsync();
+            for (int c = 0; c < 6; ++c) nb[6 * j + c] = acc[c];
+          }
+          rsync();
+        };
         bool sweep = !ZC;
         if constexpr (ZC && RING != 2) {   // the one-wave kernels
           // z = s - S r streamed column by column, each lane's ZE entries
@@ -1266,8 +1273,17 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
             if (ai < q) tz = max(tz, stage_top(act[ai]));
           }
           if constexpr (PART == 2) RS_CNT(13, 1);
+          nz_to_nb();
           hinv(zv, wave_imax63(tz));
           zn = vdot(nb, zv);
+          // NB back to n_p for the next pass of the inner loop
+          for (int j = lane; j < N; j += RT) {
+            double acc[6] = {0, 0, 0, 0, 0, 0};
+            add_coef(p, j, 1.0, acc);
+#pragma unroll
+            for (int c = 0; c < 6; ++c) nb[6 * j + c] = acc[c];
+          }
+          rsync();
         }
         zsrc = zv;
       }
