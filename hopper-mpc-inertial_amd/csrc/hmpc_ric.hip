@@ -1212,27 +1212,31 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
               za[e] = sv[ic];
               zb2[e] = 0.0;
             }
-            int a0 = 0;
-            for (; a0 + 4 <= q; a0 += 4) {
-              const double r0 = cbv[a0], r1 = cbv[a0 + 1], r2 = cbv[a0 + 2], r3 = cbv[a0 + 3];
-              double c[ZE][4];
+            // whole batches of KB columns, the last one padded by a repeated
+            // column with coefficient 0: one memory round trip per batch
+            // (round 6: the one-column tail loop waited for up to 3 serial
+            // round trips per iteration; N = 60 B = 4096: the z phase 218 k ->
+            // 67 k cycles per instance, 1.83 -> 1.96 M solves/s; 4-column
+            // padded batches 1.94 M.  The two-wave kernels' per-entry loop
+            // with a padded tail measured no gain at N = 20)
+            constexpr int KB = 8;
+            for (int a0 = 0; a0 < q; a0 += KB) {
+              double rr[KB], c[ZE][KB];
 #pragma unroll
-              for (int e = 0; e < ZE; ++e) {
+              for (int t = 0; t < KB; ++t) {
+                const int a = a0 + t < q ? a0 + t : q - 1;
+                rr[t] = a0 + t < q ? cbv[a] : 0.0;
 #pragma unroll
-                for (int t = 0; t < 4; ++t) c[e][t] = sc[e][(int64_t)(a0 + t) * NV];
+                for (int e = 0; e < ZE; ++e) c[e][t] = sc[e][(int64_t)a * NV];
               }
 #pragma unroll
               for (int e = 0; e < ZE; ++e) {
-                za[e] = fma(-r0, c[e][0], za[e]);
-                zb2[e] = fma(-r1, c[e][1], zb2[e]);
-                za[e] = fma(-r2, c[e][2], za[e]);
-                zb2[e] = fma(-r3, c[e][3], zb2[e]);
-              }
-            }
-            for (; a0 < q; ++a0) {
-              const double r0 = cbv[a0];
 #pragma unroll
-              for (int e = 0; e < ZE; ++e) za[e] = fma(-r0, sc[e][(int64_t)a0 * NV], za[e]);
+                for (int t = 0; t < KB; t += 2) {
+                  za[e] = fma(-rr[t], c[e][t], za[e]);
+                  zb2[e] = fma(-rr[t + 1], c[e][t + 1], zb2[e]);
+                }
+              }
             }
 #pragma unroll
             for (int e = 0; e < ZE; ++e) {
@@ -1347,6 +1351,7 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
       {
         const int k = uni(kdrop);
         const int idk = act[k];
+        RS_CNT(15, (1LL << 32) + (q - k - 1));   // (stamped builds: drops, cached columns shifted)
         if (lane == (idk >> 2) / 6) amask &= ~(1 << (4 * ((idk >> 2) % 6) + (idk & 3)));
         if constexpr (ZC)   // the cached columns follow the active order
           for (int m = k; m + 1 < q; ++m)

@@ -43,12 +43,15 @@ def main():
     for _ in range(3):
         out = ctx.solve_device(d['x_in'], d['x_lin'], d['x_ref'], d['pf'], d['C'], mu=d['mu'])
     torch.cuda.synchronize()
-    st = out['x'].view(torch.int64).reshape(B, -1)[:, :len(NAMES)].cpu().numpy().astype(np.float64)
+    raw = out['x'].view(torch.int64).reshape(B, -1)[:, :16].cpu().numpy()
+    st = raw[:, :len(NAMES)].astype(np.float64)
     names = NAMES if N <= 24 else NAMES[:11] + ['count_s_sweep_pairs', 'count_mrhs_cache_hits',
                                                  'count_z_fallback_sweeps', 'count_rhs_in_sweep_pairs']
     res = {n: float(st[:, i].mean()) for i, n in enumerate(names)}
     if N > 24:   # the factorisation kernel ran separately: slots 11-14 are event counts
         res['count_z_fallback_sweeps_max'] = float(st[:, 13].max())
+    res['count_drops'] = float((raw[:, 15] >> 32).mean())
+    res['count_columns_shifted'] = float((raw[:, 15] & 0xffffffff).mean())
     res['iters_mean'] = float(out['iters'].float().mean())
     res['config'] = f'{var} N={N} B={B} {" ".join(flags)}'
     print(json.dumps(res))
