@@ -234,11 +234,30 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
   // src/robotrunner.py:228-230); x_lin rows per shift_mode (3f :50-62)
   const double* xrf = a.x_ref + b * a.xref_bs;
   const double mu = a.mu ? a.mu[b] : a.mu_default;
+  // x_ref (12 N) into the union; with a compile-time horizon every load of
+  // the lane is issued before its first store (round 6: the loop's load ->
+  // store pairs were 12 serial round trips at N = 60)
+  auto stage_xref = [&]() __attribute__((always_inline)) {
+    if constexpr (NC > 0 && RING == 3) {   // (the one-wave kernels: registers to spare)
+      constexpr int XE = (12 * NC + RT - 1) / RT;
+      double xv[XE];
+#pragma unroll
+      for (int e = 0; e < XE; ++e) {
+        const int i = lane + RT * e < 12 * NC ? lane + RT * e : 0, r = i / 12, c = i - 12 * r;
+        xv[e] = xrf[(int64_t)r * a.xref_rs + c];
+      }
+#pragma unroll
+      for (int e = 0; e < XE; ++e)
+        if (lane + RT * e < 12 * NC) un[lane + RT * e] = xv[e];
+    } else {
+      for (int i = lane; i < 12 * N; i += RT) {
+        const int r = i / 12, c = i - 12 * r;
+        un[i] = xrf[(int64_t)r * a.xref_rs + c];
+      }
+    }
+  };
   if (lane < 12) xin[lane] = a.x_in[b * 12 + lane];
-  for (int i = lane; i < 12 * N; i += RT) {
-    const int r = i / 12, c = i - 12 * r;
-    un[i] = xrf[(int64_t)r * a.xref_rs + c];
-  }
+  stage_xref();
   for (int k = lane; k < N; k += RT) {
     cc[k] = a.C[b * a.C_bs + k];
     const double* row;
@@ -726,33 +745,38 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
       wsync();
     }
     // ---- w_j = G_j^-1 mu_j = Dinv'(Dinv mu_j) (lane-per-stage; 0 beyond jt)
-    const int nitem = (MR ? nr : 1) * (jt + 1);
-    for (int it = lane; it < nitem; it += RT) {
-      const int r_ = MR ? it / (jt + 1) : 0, j = it - r_ * (jt + 1);
-      double* mcol = mu_;
-      if constexpr (MR) mcol = r_ == 0 ? c0 : r_ == 1 ? c1 : r_ == 2 ? c2 : c3;
-      double mv[6], y[6], w[6], g[21];
+    // lane j holds stage j (jt < kRicNmax = 64): its Dinv is loaded once,
+    // one round trip, for every row (round 6: one item per (row, stage)
+    // reloaded Dinv per row, up to four serial round trips at N = 60)
+    const int nrows = MR ? nr : 1;
+    for (int j = lane; j <= jt; j += RT) {
+      double g[21];
       const double* gj = gi + 21 * j;
 #pragma unroll
       for (int e = 0; e < 21; ++e) g[e] = gj[e];
+      for (int r_ = 0; r_ < nrows; ++r_) {
+        double* mcol = mu_;
+        if constexpr (MR) mcol = r_ == 0 ? c0 : r_ == 1 ? c1 : r_ == 2 ? c2 : c3;
+        double mv[6], y[6], w[6];
 #pragma unroll
-      for (int c = 0; c < 6; ++c) mv[c] = mcol[6 * j + c];
+        for (int c = 0; c < 6; ++c) mv[c] = mcol[6 * j + c];
 #pragma unroll
-      for (int c = 0; c < 6; ++c) {   // y = Dinv mu (lower)
-        double s = 0.0;
+        for (int c = 0; c < 6; ++c) {   // y = Dinv mu (lower)
+          double s = 0.0;
 #pragma unroll
-        for (int d = 0; d <= c; ++d) s = fma(g[loff(c) + d], mv[d], s);
-        y[c] = s;
+          for (int d = 0; d <= c; ++d) s = fma(g[loff(c) + d], mv[d], s);
+          y[c] = s;
+        }
+#pragma unroll
+        for (int c = 0; c < 6; ++c) {   // w = Dinv' y
+          double s = 0.0;
+#pragma unroll
+          for (int d = c; d < 6; ++d) s = fma(g[loff(d) + c], y[d], s);
+          w[c] = s;
+        }
+#pragma unroll
+        for (int c = 0; c < 6; ++c) mcol[6 * j + c] = w[c];
       }
-#pragma unroll
-      for (int c = 0; c < 6; ++c) {   // w = Dinv' y
-        double s = 0.0;
-#pragma unroll
-        for (int d = c; d < 6; ++d) s = fma(g[loff(d) + c], y[d], s);
-        w[c] = s;
-      }
-#pragma unroll
-      for (int c = 0; c < 6; ++c) mcol[6 * j + c] = w[c];
     }
     if constexpr (MR) gsync();
     else wsync();
@@ -1021,7 +1045,19 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
       if (hit) {
         if constexpr (PART == 2) RS_CNT(12, 1);
         const double* col = gcache + (int64_t)__builtin_ctzll(hit) * NV;
-        for (int i = lane; i < NV; i += RT) sv[i] = col[i];
+        if constexpr (NC > 0) {
+          // every load of the column in flight before the first store (round
+          // 6: the loop's load -> store pairs were serial round trips)
+          constexpr int CE = (6 * NC + RT - 1) / RT;
+          double cv[CE];
+#pragma unroll
+          for (int e = 0; e < CE; ++e) cv[e] = col[lane + RT * e < NV ? lane + RT * e : 0];
+#pragma unroll
+          for (int e = 0; e < CE; ++e)
+            if (lane + RT * e < NV) sv[lane + RT * e] = cv[e];
+        } else {
+          for (int i = lane; i < NV; i += RT) sv[i] = col[i];
+        }
         wsync();
       } else {
         // candidates: each stage's most violated constraint (lanes < N), not
@@ -1411,10 +1447,7 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
     return;
   }
   // x_ref into the union again (over the dead R), x* staged over SV..
-  for (int i = lane; i < 12 * N; i += RT) {
-    const int r = i / 12, c = i - 12 * r;
-    un[i] = xrf[(int64_t)r * a.xref_rs + c];
-  }
+  stage_xref();
   for (int i = lane; i < NV; i += RT) {
     const int j = i / 6, c = i - 6 * j;
     const bool fr = c >= 3 || (cc[j] != 0.0 && !(VAR == 2 && c == 1));
@@ -1492,19 +1525,38 @@ __global__ void __launch_bounds__(RT) __attribute__((amdgpu_waves_per_eu(OCC, OC
   double* kw = a.kws + (int64_t)blockIdx.x * a.kws_stride;
   while (true) {
     int b = 0;
-    if (threadIdx.x == 0) {
-      b = atomicAdd(a.work, 1);
-      if (a.list && b < a.B) {   // longest-first queue: ticket b in the stance buckets, highest first
+    if constexpr (OCC == 1) {
+      if (threadIdx.x == 0) b = atomicAdd(a.work, 1);
+      // longest-first queue: ticket b in the stance buckets, highest first;
+      // the bucket counts load beside the ticket, one per lane (round 6:
+      // lane 0 walked them one serial round trip per bucket; the 2-wave
+      // kernels keep that form, whose registers sit at the 256 cap)
+      const int bc = a.list && (int)threadIdx.x < a.split_nbkt ? a.list_count[threadIdx.x] : 0;
+      b = __builtin_amdgcn_readfirstlane(b);
+      if (a.list && b < a.B) {
         int s = a.split_nbkt - 1;
         for (; s > 0; --s) {
-          const int c = a.list_count[s];
+          const int c = __builtin_amdgcn_readlane(bc, s);
           if (b < c) break;
           b -= c;
         }
         b = a.list[(int64_t)s * a.B + b];
       }
+    } else {
+      if (threadIdx.x == 0) {
+        b = atomicAdd(a.work, 1);
+        if (a.list && b < a.B) {   // longest-first queue: ticket b in the stance buckets, highest first
+          int s = a.split_nbkt - 1;
+          for (; s > 0; --s) {
+            const int c = a.list_count[s];
+            if (b < c) break;
+            b -= c;
+          }
+          b = a.list[(int64_t)s * a.B + b];
+        }
+      }
+      b = __builtin_amdgcn_readfirstlane(b);
     }
-    b = __builtin_amdgcn_readfirstlane(b);
     if (b >= a.B) break;
     double* kwi = PART == 2 ? a.kinst + (int64_t)b * a.kinst_stride : kw;
     ric_solve<VAR, 1, OCC == 2 ? kRing2Wave : kRing1Wave, true, NC, CAPC, PART>(a, N, (int64_t)b, ric_sm, ric_sm + L.RM,
