@@ -46,7 +46,8 @@ struct hmpc_ctx {
   // solve whose overflow pass -- which zeroes them at its end -- did not run)
   bool ovf_dirty = true;
   bool ovf_total_failed = false;
-  bool ovf2_zeroed = false;   // the second overflow header (run_solve) is zero   // the diagnostic counter could not be allocated
+  bool ovf2_zeroed = false;
+  int ric_cap_last = 0;   // the Riccati main pass's active-set capacity in the last solve (0: none yet)   // the second overflow header (run_solve) is zero   // the diagnostic counter could not be allocated
   double* rws = nullptr;
   // dense split launch: the three class lists [3][split_cap], or (longest-first
   // order) up to N + 1 stance-count buckets of split_cap entries; the Riccati
@@ -328,6 +329,7 @@ int prepare_ric(hmpc_ctx* c, int64_t B, hmpc::SolveArgs& a) {
       }
     }
     c->ric_fused = hmpc::ric_occ(c->N) == 1 && a.kinst == nullptr;
+    c->ric_cap_last = a.kinst ? hmpc::ric_qcap_batch(c->N, B) : hmpc::ric_qcap(c->N);
     // the longest-first work queue: stance-count buckets (<= 13 counters in
     // the overflow header), lists of B entries each
     const int nb = hmpc::ric_lpt_buckets(c->N);
@@ -546,8 +548,8 @@ int hmpc_active_capacity(hmpc_ctx* c) {
       return hmpc::dense_qmax(c->N, 1);
     case hmpc::Kernel::DenseF32R:
       return hmpc::dense_qmax(c->N, 2);
-    case hmpc::Kernel::Riccati:
-      return hmpc::ric_qcap(c->N);
+    case hmpc::Kernel::Riccati:   // (of the last solve: N = 60 small batches run capacity 64)
+      return c->ric_cap_last ? c->ric_cap_last : hmpc::ric_qcap(c->N);
     case hmpc::Kernel::Cas:
       return 18 * c->N;
     case hmpc::Kernel::Wide:
@@ -589,6 +591,9 @@ const char* hmpc_kernel_name(hmpc_ctx* c) {
         if (hmpc::ric_static_n(c->N) == 60) return v3 ? "hmpc::ric_kernel<3, 1, 60, 47, 0>" : "hmpc::ric_kernel<2, 1, 60, 47, 0>";
         return v3 ? "hmpc::ric_kernel<3, 1, 0, 0, 0>" : "hmpc::ric_kernel<2, 1, 0, 0, 0>";
       }
+      if (hmpc::ric_static_n(c->N) == 60 && c->ric_cap_last == 64)   // the last solve's small batch
+        return v3 ? "hmpc::ric_factor_kernel<3, 60, 47> + hmpc::ric_kernel<3, 1, 60, 64, 2>"
+                  : "hmpc::ric_factor_kernel<2, 60, 47> + hmpc::ric_kernel<2, 1, 60, 64, 2>";
       if (hmpc::ric_static_n(c->N) == 60)
         return v3 ? "hmpc::ric_factor_kernel<3, 60, 47> + hmpc::ric_kernel<3, 1, 60, 47, 2>"
                   : "hmpc::ric_factor_kernel<2, 60, 47> + hmpc::ric_kernel<2, 1, 60, 47, 2>";

@@ -114,6 +114,9 @@ constexpr int ST_OVERFLOW = 4;   // internal: re-solved by the overflow pass
 // ric_kernel<VAR, 2>) with capacity >= 32, else 4 workgroups per CU (1 wave /
 // SIMD).  Larger active sets go to the overflow pass.
 int ric_qcap(int N);
+// ... for a batch of B instances (the Runner's N = 60 at small batches runs a
+// capacity-64 solve kernel, hmpc_ric.hip)
+int ric_qcap_batch(int N, int64_t B);
 int ric_occ(int N);
 // the compile-time horizon the Riccati kernel for N runs with (0: runtime N)
 int ric_static_n(int N);

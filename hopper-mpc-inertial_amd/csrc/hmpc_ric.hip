@@ -1734,10 +1734,33 @@ int ric_static_n(int N) {
   return 0;
 }
 
+// The Runner's horizon at small batches (round 6): the solve kernel with R's
+// capacity 64 (48.8 KB of LDS, 3 workgroups per CU) when every instance
+// gets its own workgroup at that occupancy anyway.  The Runner's own
+// trajectory (the reference's configs[0] run) has calls with 48-59 active
+// rows, which capacity 47 handed to the generic capacity-6N overflow pass at
+// ~7 ms each: 41 of the single robot's 108 ms per run.
+constexpr int kSmallCap60 = 64;
+int ric_cus() {
+  static const int cus = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return 0;
+    return n;
+  }();
+  return cus;
+}
+int ric_qcap_batch(int N, int64_t B) {
+  if (ric_static_n(N) == 60 && B <= 3 * (int64_t)ric_cus() && ric_kinst_stride(N, B) > 0) return kSmallCap60;
+  return ric_qcap(N);
+}
+
 // K / Dinv of every stage, then the cached columns H^-1 n_a (capacity x NV),
 // then the MRHS candidate columns (kNSC x NV)
 int64_t ric_kws_stride(int N) {
-  return ric_kws_doubles(N) + (((((int64_t)ric_qcap(N) + kNSC) * 6 * N) + 15) & ~(int64_t)15);
+  const int cap = ric_static_n(N) == 60 ? kSmallCap60 : ric_qcap(N);
+  return ric_kws_doubles(N) + (((((int64_t)cap + kNSC) * 6 * N) + 15) & ~(int64_t)15);
 }
 
 int64_t ric_rws_stride(int N) {
@@ -1773,6 +1796,9 @@ bool ric_launch(int N, const SolveArgs& a, hipStream_t s, int* per) {
   const int cap = ric_qcap(N);
   if (a.kinst && !per) {   // factorisation kernel, then the solve kernel without phase 2
     if constexpr (OCC == 1) {
+      if (ric_static_n(N) == 60 && ric_qcap_batch(N, a.B) == kSmallCap60)   // small batches: capacity 64
+        return ric_launch_fac(ric_factor_kernel<VAR, 60, 47>, N, cap, a, s) &&
+               ric_launch_k(ric_kernel<VAR, OCC, 60, kSmallCap60, 2>, N, kSmallCap60, a, s, per);
       if (ric_static_n(N) == 60)
         return ric_launch_fac(ric_factor_kernel<VAR, 60, 47>, N, cap, a, s) &&
                ric_launch_k(ric_kernel<VAR, OCC, 60, 47, 2>, N, cap, a, s, per);

@@ -12,6 +12,7 @@
 #   bench:TAG:ARGS              bench.py ARGS > OUT/bench_TAG.json
 #   trace:TAG:ARGS              rocprofv3 --kernel-trace --stats of bench.py ARGS
 #   runner                      tools/runner_time.py, eager and graph replay
+#   runnertrace                 rocprofv3 kernel trace of one robot's run (graph replay)
 #   stamps:TAG:LIB:ENV          tools/phase_stamps.py with HMPC_LIB=LIB and ENV
 #                               (NAME=VALUE pairs)
 #   ricstamps:TAG:LIB:ARGS      tools/ric_stamps.py ARGS with HMPC_LIB=LIB
@@ -47,6 +48,11 @@ for step in "$@"; do
       timeout -k 10 300 python tools/runner_time.py > $OUT/runner_eager.json 2>&1 || { echo "runner eager failed"; exit 1; }
       timeout -k 10 300 python tools/runner_time.py graph > $OUT/runner_graph.json 2>&1 || { echo "runner graph failed"; exit 1; }
       tail -c 400 $OUT/runner_graph.json; echo ;;
+    runnertrace)
+      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $OUT/runnertrace -o run -- \
+        python3 $R/tools/runner_time.py graph 1 > $OUT/runnertrace.log 2>&1); rc=$?
+      stop $rc; [ $rc -eq 0 ] || { echo "runnertrace failed"; exit 1; }
+      find $OUT/runnertrace -name "*kernel_stats.csv" -exec cut -d, -f1-5 {} \; | head -14 ;;
     stamps)
       envs=$(sp $a3)
       env HMPC_LIB=hopper-mpc-inertial_amd/$a2 $envs timeout -k 10 180 python tools/phase_stamps.py \

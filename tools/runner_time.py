@@ -1,8 +1,8 @@
 """Wall time of the device Runner (hmpc_runner.Runner.run: plan + gait +
 100 MPC periods of mpcontrol_plan + plant) for the reference's configs[0]
 (run.py 3f --N_run=2000, N = 60) at batch 1 and a few batch sizes.
-python tools/runner_time.py [graph]     (graph: timed run = a replay of the
-captured run, hmpc_runner.Runner.run(graph=True))"""
+python tools/runner_time.py [graph] [B ...]     (graph: timed run = a replay of the
+captured run, hmpc_runner.Runner.run(graph=True); robot counts, default 1 256 4096)"""
 import json
 import os
 import sys
@@ -17,7 +17,8 @@ import hmpc_runner  # noqa: E402
 
 graph = 'graph' in sys.argv[1:]
 res = {}
-for B in (1, 256, 4096):
+batches = [int(x) for x in sys.argv[1:] if x.isdigit()] or [1, 256, 4096]
+for B in batches:
     r = hmpc_runner.Runner(dt=1e-3, dyn='3f', curve=False, N_run=2000, N=60, batch=B)
     kw = dict(record=False)
     if graph:
