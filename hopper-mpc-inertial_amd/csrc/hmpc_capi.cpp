@@ -45,9 +45,9 @@ struct hmpc_ctx {
   // the counters need a zeroing before the next solve (fresh buffer, or a
   // solve whose overflow pass -- which zeroes them at its end -- did not run)
   bool ovf_dirty = true;
-  bool ovf_total_failed = false;
-  bool ovf2_zeroed = false;
-  int ric_cap_last = 0;   // the Riccati main pass's active-set capacity in the last solve (0: none yet)   // the second overflow header (run_solve) is zero   // the diagnostic counter could not be allocated
+  bool ovf_total_failed = false;   // the diagnostic counter could not be allocated
+  bool ovf2_zeroed = false;   // the second overflow header (run_solve) is zero
+  int ric_cap_last = 0;   // the Riccati main pass's active-set capacity in the last solve (0: none yet)
   double* rws = nullptr;
   // dense split launch: the three class lists [3][split_cap], or (longest-first
   // order) up to N + 1 stance-count buckets of split_cap entries; the Riccati
@@ -115,7 +115,7 @@ hmpc::SolveArgs make_args(hmpc_ctx* c, int64_t B, const double* x_in, const doub
   a.ovf_count = nullptr; a.ovf_list = nullptr; a.rws = nullptr; a.rws_stride = 0;
   a.ovf_total = nullptr;
   a.ovf_hdr1 = nullptr;
-  a.work = nullptr; a.kws = nullptr; a.kws_stride = 0; a.ric_groups = 0;
+  a.work = nullptr; a.work_bound = nullptr; a.kws = nullptr; a.kws_stride = 0; a.ric_groups = 0;
   a.kinst = nullptr; a.kinst_stride = 0;
   a.split_count = nullptr; a.split_list = nullptr; a.list = nullptr; a.list_count = nullptr;
   a.lpt = 0; a.lpt_lo = 0; a.lpt_hi = -1; a.split_nbkt = 0;
@@ -216,7 +216,7 @@ int ensure_split(hmpc_ctx* c, int64_t B, int nlist, const char* what) {
 int prepare_ric(hmpc_ctx* c, int64_t B, hmpc::SolveArgs& a) {
   const hmpc::Kernel k = hmpc::pick_kernel(c->variant, c->N, c->precision);
   a.ovf_count = nullptr; a.ovf_list = nullptr; a.rws = nullptr; a.rws_stride = 0;
-  a.work = nullptr; a.kws = nullptr; a.kws_stride = 0; a.ric_groups = 0;
+  a.work = nullptr; a.work_bound = nullptr; a.kws = nullptr; a.kws_stride = 0; a.ric_groups = 0;
   a.kinst = nullptr; a.kinst_stride = 0;
   a.split_count = nullptr; a.split_list = nullptr;
   if (k == hmpc::Kernel::Cas) {   // instance counter + R slots, no overflow pass
@@ -346,7 +346,8 @@ int prepare_ric(hmpc_ctx* c, int64_t B, hmpc::SolveArgs& a) {
   return HMPC_OK;
 }
 
-// The second overflow header and list (run_solve, HMPC_PREC_F32_REFINED)
+// The second overflow header and list (run_solve: HMPC_PREC_F32_REFINED's
+// fp64 fallback pass, the N = 60 second tier)
 int32_t* ovf_hdr2(hmpc_ctx* c) { return c->ovf + kOvfHeader + c->ovf_cap; }
 
 // One solve pass over the batch: the main kernel, then (dense / Riccati
@@ -366,12 +367,16 @@ int run_solve(hmpc_ctx* c, hmpc::SolveArgs a, hipStream_t s) {
   // every main pass that has one, zeroes them at its end (stream order: the
   // next solve's kernels see them zero).  The CasADi kernel has no overflow
   // pass.
-  const bool fb = a.ovf_count && hmpc::pick_kernel(c->variant, c->N, c->precision) == hmpc::Kernel::DenseF32R;
+  const hmpc::Kernel kk = hmpc::pick_kernel(c->variant, c->N, c->precision);
+  const bool fb = a.ovf_count && kk == hmpc::Kernel::DenseF32R;
+  // N = 60 at the large-batch capacity: the capacity-64 kernel takes the
+  // overflow list first (the Runner's robots share their 48-59-row calls)
+  const bool t2 = a.ovf_count && kk == hmpc::Kernel::Riccati && a.kinst && hmpc::ric_has_tier2(c->N, a.B);
   if (a.work && (!a.ovf_count || c->ovf_dirty)) {
     hipError_t e = hipMemsetAsync(a.work - 1, 0, (a.ovf_count ? kOvfHeader : 3) * sizeof(int32_t), s);
     if (e != hipSuccess) return fail_hip(c, e, "hipMemsetAsync(overflow count)");
   }
-  if (fb && (!c->ovf2_zeroed || c->ovf_dirty)) {   // (the generic pass zeroes it at its end)
+  if ((fb || t2) && (!c->ovf2_zeroed || c->ovf_dirty)) {   // (the generic pass zeroes it at its end)
     hipError_t e = hipMemsetAsync(ovf_hdr2(c), 0, kOvfHeader * sizeof(int32_t), s);
     if (e != hipSuccess) return fail_hip(c, e, "hipMemsetAsync(second overflow count)");
     c->ovf2_zeroed = true;
@@ -395,6 +400,28 @@ int run_solve(hmpc_ctx* c, hmpc::SolveArgs a, hipStream_t s) {
     f.ovf_list = ovf_hdr2(c) + kOvfHeader;
     if (!hmpc::launch_solve_fp64_list(c->variant, c->N, f, s)) {
       c->err = "fp64 fallback pass launch";
+      return HMPC_ERR_UNSUPPORTED;
+    }
+    hmpc::SolveArgs o = a;   // the generic pass over what that kernel handed on
+    o.ovf_count = f.ovf_count;
+    o.ovf_list = f.ovf_list;
+    o.ovf_hdr1 = a.ovf_count;
+    if (!hmpc::launch_solve_ric_overflow(c->variant, c->N, o, kOvfGroups, s)) {
+      c->err = "overflow pass launch";
+      return HMPC_ERR_UNSUPPORTED;
+    }
+  } else if (t2) {
+    hmpc::SolveArgs f = a;   // the capacity-64 solve kernel over the main pass's overflow list
+    f.list = a.ovf_list;
+    f.list_count = a.ovf_count;
+    f.work_bound = a.ovf_count;
+    f.split_nbkt = 1;
+    f.lpt = 0;
+    f.work = ovf_hdr2(c) + 1;
+    f.ovf_count = ovf_hdr2(c);
+    f.ovf_list = ovf_hdr2(c) + kOvfHeader;
+    if (!hmpc::launch_solve_ric_tier2(c->variant, c->N, f, s)) {
+      c->err = "second-tier pass launch";
       return HMPC_ERR_UNSUPPORTED;
     }
     hmpc::SolveArgs o = a;   // the generic pass over what that kernel handed on

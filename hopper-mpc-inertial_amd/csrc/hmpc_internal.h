@@ -69,6 +69,8 @@ struct SolveArgs {
   // Riccati kernel (persistent): instance counter (zeroed before the launch),
   // resident workgroups and their K / Dinv workspace (kws_stride doubles each)
   int32_t* work;
+  // the number of tickets (instances of a.list) when shorter than B, or nullptr
+  const int32_t* work_bound;
   int ric_groups;
   double* kws;
   int64_t kws_stride;
@@ -137,6 +139,11 @@ bool launch_solve_ric(int variant, int N, const SolveArgs& a, hipStream_t stream
 // count) over a.list / *a.list_count, one workgroup per entry, grid a.B; false
 // when no dense fp64 object serves N.  HMPC_PREC_F32_REFINED's fallback pass.
 bool launch_solve_fp64_list(int variant, int N, const SolveArgs& a, hipStream_t s);
+// N = 60 with the large-batch capacity (47): a second-tier pass of the
+// capacity-64 solve kernel over the main pass's overflow list (a.list, count
+// *a.work_bound, its own ticket counter a.work) before the generic pass
+bool ric_has_tier2(int N, int64_t B);
+bool launch_solve_ric_tier2(int variant, int N, const SolveArgs& a, hipStream_t s);
 // the overflow pass over a.ovf_list (count on the device), <= groups workgroups
 bool launch_solve_ric_overflow(int variant, int N, const SolveArgs& a, int groups, hipStream_t s);
 

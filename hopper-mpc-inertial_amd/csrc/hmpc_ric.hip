@@ -1532,8 +1532,12 @@ __global__ void __launch_bounds__(RT) __attribute__((amdgpu_waves_per_eu(OCC, OC
       // lane 0 walked them one serial round trip per bucket; the 2-wave
       // kernels keep that form, whose registers sit at the 256 cap)
       const int bc = a.list && (int)threadIdx.x < a.split_nbkt ? a.list_count[threadIdx.x] : 0;
+      // (a.work_bound: the tickets of a list shorter than the batch -- the
+      // N = 60 second-tier pass over the main pass's overflow list)
+      const int bound = a.work_bound ? *a.work_bound : (int)a.B;
       b = __builtin_amdgcn_readfirstlane(b);
-      if (a.list && b < a.B) {
+      if (b >= bound) break;
+      if (a.list) {
         int s = a.split_nbkt - 1;
         for (; s > 0; --s) {
           const int c = __builtin_amdgcn_readlane(bc, s);
@@ -1741,6 +1745,7 @@ int ric_static_n(int N) {
 // rows, which capacity 47 handed to the generic capacity-6N overflow pass at
 // ~7 ms each: 41 of the single robot's 108 ms per run.
 constexpr int kSmallCap60 = 64;
+
 int ric_cus() {
   static const int cus = [] {
     int dev = 0, n = 0;
@@ -1789,6 +1794,23 @@ bool ric_launch_fac(K kern, int N, int cap, const SolveArgs& a, hipStream_t s) {
   const size_t lds = (size_t)RicLay(N, cap, false, true).total * sizeof(double);
   if (!set_lds(kern, lds)) return false;
   hipLaunchKernelGGL(kern, dim3((unsigned)a.B), dim3(RT), lds, s, a, N, cap);
+  return true;
+}
+// the N = 60 second-tier pass: the capacity-64 solve kernel over a list
+// (a.list, count *a.work_bound), persistent workgroups that take its entries
+// off their own counter (a.work)
+template <int VAR>
+bool ric_launch_tier2(int N, const SolveArgs& a, hipStream_t s) {
+  if (ric_static_n(N) != 60 || !a.kinst || !a.list || !a.work_bound) return false;
+  auto kern = ric_kernel<VAR, 1, 60, kSmallCap60, 2>;
+  const size_t lds = ric_lds_bytes(N, kSmallCap60);
+  if (!set_lds(kern, lds)) return false;
+  // every workgroup resident at once (3 per CU): the list is usually empty
+  // (each group reads the bound and exits), but when many instances share a
+  // hard call -- the Runner's robots in step -- it is most of the batch
+  const int64_t g3 = 3 * (int64_t)(ric_cus() > 0 ? ric_cus() : 256);
+  const int64_t g = a.B < g3 ? a.B : g3;
+  hipLaunchKernelGGL(kern, dim3((unsigned)g), dim3(RT), lds, s, a, N, kSmallCap60);
   return true;
 }
 template <int VAR, int OCC>
@@ -1868,6 +1890,12 @@ bool launch_solve_ric(int variant, int N, const SolveArgs& a, hipStream_t s) {
   SolveArgs a0 = a;
   a0.list = nullptr;
   return ric_launch_any(variant, N, a0, s, nullptr);
+}
+
+bool ric_has_tier2(int N, int64_t B) { return ric_static_n(N) == 60 && ric_qcap_batch(N, B) < kSmallCap60; }
+bool launch_solve_ric_tier2(int variant, int N, const SolveArgs& a, hipStream_t s) {
+  if (a.B <= 0) return true;
+  return variant == 3 ? ric_launch_tier2<3>(N, a, s) : variant == 2 ? ric_launch_tier2<2>(N, a, s) : false;
 }
 
 bool launch_solve_ric_overflow(int variant, int N, const SolveArgs& a, int groups, hipStream_t s) {

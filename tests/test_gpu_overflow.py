@@ -180,3 +180,35 @@ def test_counters_reset_between_solves(hm, N):
         for k in ('u', 'obj', 'status'):
             assert np.array_equal(r[k], fresh[name][k]), (name, fn.__name__, k)
     cx.close()
+
+
+def test_overflow_n60_second_tier(hm):
+    """A large N = 60 batch (B = 1024: the capacity-47 solve kernel, 4 groups
+    per CU) whose main pass overflows: the capacity-64 kernel re-solves the
+    overflow list first (round 6), the generic capacity-6N pass only what
+    outgrows 64.  Every instance equals the port; the adversarial ones span
+    both tiers (active sets 61-94 of the reference-form rows)."""
+    import hmpc_plan
+    from oracle import port
+    N, B, A = 60, 1024, 24
+    inst = hmpc_plan.sample_instances(B - A, N, curve=False, seed=61)
+    adv = adversarial(A, N, 2, 12.0, 2.0)
+    inst = {k: np.concatenate([inst[k], adv[k]]) for k in inst}
+    c = hmpc_plan.runner_constants()
+    cx = hm.Context('3f', N, t=c['t'], m=c['m'], g=c['g'], mu=1.0, Jinv=c['Jinv'], rh=c['rh'])
+    t0 = cx.overflow_total
+    gpu = cx.solve_host(inst['x_in'], inst['x_lin'], inst['x_ref'], inst['pf'], inst['C'], mu=inst['mu'])
+    handed = cx.overflow_total - t0
+    assert cx.kernel_name == 'hmpc::ric_factor_kernel<3, 60, 47> + hmpc::ric_kernel<3, 1, 60, 47, 2>'
+    assert cx.active_capacity == 47
+    cx.close()
+    ref = port.solve_batch('3f', N, inst['x_in'], inst['x_lin'], inst['x_ref'], inst['pf'], inst['C'],
+                           mu=inst['mu'], nthreads=16)
+    assert np.array_equal(gpu['status'], ref['status'])
+    ok = ref['status'] == 0
+    assert ok[B - A:].all()
+    assert np.abs(gpu['u'][ok] - ref['u'][ok]).max() <= U_TOL
+    assert np.abs(gpu['x'][ok] - ref['x'][ok]).max() <= U_TOL
+    rel = np.abs(gpu['obj'][ok] - ref['obj'][ok]) / np.maximum(np.abs(ref['obj'][ok]), 1.0)
+    assert rel.max() <= 1e-8
+    assert handed >= A, handed   # every adversarial instance left the main pass

@@ -50,7 +50,7 @@ for step in "$@"; do
       tail -c 400 $OUT/runner_graph.json; echo ;;
     runnertrace)
       (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $OUT/runnertrace -o run -- \
-        python3 $R/tools/runner_time.py graph 1 > $OUT/runnertrace.log 2>&1); rc=$?
+        python3 $R/tools/runner_time.py graph ${RUNNER_B:-1} > $OUT/runnertrace.log 2>&1); rc=$?
       stop $rc; [ $rc -eq 0 ] || { echo "runnertrace failed"; exit 1; }
       find $OUT/runnertrace -name "*kernel_stats.csv" -exec cut -d, -f1-5 {} \; | head -14 ;;
     stamps)
