@@ -1232,7 +1232,10 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
           rsync();
         };
         bool sweep = !ZC;
-        if constexpr (ZC && RING != 2) {   // the one-wave kernels
+        // the batched form: the one-wave kernels, and (round 6) the 3f
+        // two-wave ones -- configs[3] 13.45 -> 13.71 M at 12 -> 20 B/lane of
+        // scratch; in the 2f two-wave kernels it spilled 32 B/lane
+        if constexpr (ZC && (RING != 2 || VAR == 3)) {   // 
           // z = s - S r streamed column by column, each lane's ZE entries
           // i = i0 + lane + 64 e side by side: 4 x ZE independent loads in flight
           // per lane per batch of 4 columns (the latency of the L2/MALL-resident
@@ -1253,9 +1256,9 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
             // (round 6: the one-column tail loop waited for up to 3 serial
             // round trips per iteration; N = 60 B = 4096: the z phase 218 k ->
             // 67 k cycles per instance, 1.83 -> 1.96 M solves/s; 4-column
-            // padded batches 1.94 M.  The two-wave kernels' per-entry loop
-            // with a padded tail measured no gain at N = 20)
-            constexpr int KB = 8;
+            // padded batches 1.94 M.  In the two-wave kernels 4-column
+            // batches of both entries per lane, ZE = 2: configs[3] +1.9 %)
+            constexpr int KB = RING == 2 ? 4 : 8;
             for (int a0 = 0; a0 < q; a0 += KB) {
               double rr[KB], c[ZE][KB];
 #pragma unroll
