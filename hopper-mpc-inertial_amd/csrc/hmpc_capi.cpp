@@ -504,7 +504,7 @@ int check_solve_args(hmpc_ctx* c, int64_t B, const void* x_in, const void* x_lin
 
 extern "C" {
 
-int hmpc_version(void) { return 10500; }
+int hmpc_version(void) { return 10501; }
 
 int hmpc_supported_horizons(int variant, int* Ns, int cap) {
   return hmpc::supported_horizons(variant, Ns, cap);

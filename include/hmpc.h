@@ -99,7 +99,9 @@ typedef struct hmpc_ctx hmpc_ctx;
    hmpc_active_capacity, hmpc_plan_batch, hmpc_gait_batch, HMPC_VARIANT_CAS;
    1.3.0 = + hmpc_solve_batch_stats, HMPC_PREC_F32_REFINED, hmpc_set_refinement;
    1.4.0 = + hmpc_set_order;
-   1.5.0 = + hmpc_overflow_total */
+   1.5.0 = + hmpc_overflow_total;
+   1.5.1 = hmpc_kernel_name / hmpc_active_capacity report the last solve's N = 60
+           kernel (capacity 64 at small batches) */
 int hmpc_version(void);
 
 /* Which horizons have a dedicated (one- or two-wavefront) kernel for
@@ -269,14 +271,19 @@ int hmpc_set_order(hmpc_ctx* ctx, int order);
    horizons above 24 run "hmpc::ric_factor_kernel<...> + hmpc::ric_kernel<..., 2>"); a split launch names
    every class kernel, "hmpc::solve_kernel<3, 10, double, 48, 13> + hmpc::solve_kernel<3, 10,
    double, 0, 0>" (the narrowest first; 2f's full class is the 5N-wide
-   "hmpc::solve_kernel<2, 10, double, 50, 20>").  Static string, "" when none.  For
+   "hmpc::solve_kernel<2, 10, double, 50, 20>"; the fp32 builds list the fp64
+   "hmpc::swing_kernel<10, 13>" class first).  N = 60 names the last solve's
+   kernel: batches up to three workgroups per CU run the capacity-64
+   "hmpc::ric_kernel<3, 1, 60, 64, 2>".  Static string, "" when none.  For
    benchmark records and profiles. */
 const char* hmpc_kernel_name(hmpc_ctx* ctx);
 
 /* Active-set capacity of that kernel's main pass (-1 when none): instances
    whose active set grows beyond it are re-solved by the overflow pass
    (capacity 6N) inside the same call, so this is a performance figure, not a
-   limit (0 for the generic kernel, which has no overflow pass). */
+   limit (0 for the generic kernel, which has no overflow pass).  N = 60: the
+   last solve's (64 for small batches, else 47, whose overflows go first to a
+   capacity-64 second tier). */
 int hmpc_active_capacity(hmpc_ctx* ctx);
 
 /* Instances the overflow pass has re-solved on this context since it was
