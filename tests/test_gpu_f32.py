@@ -142,11 +142,14 @@ def test_fp32_refined_contracts(hm, k, bound):
     assert np.abs(g['u'][ok] - ref['u'][ok]).max() <= bound
 
 
-def test_fp32_refined_unconverged_goes_to_fp64(hm):
+@pytest.mark.parametrize('k', [0, 1])
+def test_fp32_refined_unconverged_goes_to_fp64(hm, k):
     """A refinement that has not converged is not reported as solved (ADVICE
     r4): with one correction the last step is far above the acceptance bound
-    (kRefineDu), so every instance is re-solved by the fp64 pass -- statuses
-    equal, |du| <= 1e-6 (one correction alone leaves ~2e-2)."""
+    (kRefineDu), and with none there is no converged step at all (ADVICE r5,
+    include/hmpc.h), so every instance is re-solved in fp64 (round 6: the
+    dense fp64 kernel over the fallback list) -- statuses equal, |du| <= 1e-6
+    (one correction alone leaves ~2e-2)."""
     import hmpc_plan
     from oracle import port
     N, B = 10, 256
@@ -154,7 +157,7 @@ def test_fp32_refined_unconverged_goes_to_fp64(hm):
     c = hmpc_plan.runner_constants()
     cx = hm.Context('3f', N, t=c['t'], m=c['m'], g=c['g'], mu=1.0, Jinv=c['Jinv'], rh=c['rh'],
                     precision='f32_refined')
-    cx.set_refinement(1)
+    cx.set_refinement(k)
     g = cx.solve_host(inst['x_in'], inst['x_lin'], inst['x_ref'], inst['pf'], inst['C'], mu=inst['mu'])
     fallbacks = cx.overflow_total   # (hmpc_overflow_total)
     cx.set_refinement(5)
