@@ -31,6 +31,7 @@ def hm():
     ('2f', 20, 2048, True, 'hmpc::ric_kernel<2, 2, 20, 38, 0>'),
     ('3f', 40, 1024, True, 'hmpc::ric_factor_kernel<3, 0, 0> + hmpc::ric_kernel<3, 1, 0, 0, 2>'),
     ('3f', 60, 1024, False, 'hmpc::ric_factor_kernel<3, 60, 47> + hmpc::ric_kernel<3, 1, 60, 47, 2>'),
+    ('2f', 60, 1024, True, 'hmpc::ric_factor_kernel<2, 60, 47> + hmpc::ric_kernel<2, 1, 60, 47, 2>'),
 ])
 def test_riccati_stress_vs_port(hm, variant, N, B, curve, kernel):
     import hmpc_plan
