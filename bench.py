@@ -261,17 +261,13 @@ def main():
     ex = hmpc_dist.ResultExchange(B, dev, counts=counts) if world > 1 else None
     last = [out]
 
-    def step(ev=None):
+    def step():
         o = out
         if ex is not None:
             ob, sb = ex.outputs()
             o = dict(out, obj=ob, status=sb)
-        if ev is not None:
-            ev[0].record(stream)
         ctx.solve_device(d['x_in'], d['x_lin'], d['x_ref'], d['pf'], d['C'], mu=d['mu'],
                          out=o, stream=stream.cuda_stream)
-        if ev is not None:
-            ev[1].record(stream)
         if ex is not None:
             ex.exchange()
         last[0] = o
@@ -291,21 +287,25 @@ def main():
     torch.cuda.synchronize(dev)
     kernel = ctx.kernel_name   # (the classes this batch's solves ran)
     ovf0 = ctx.overflow_total   # instances the overflow pass re-solved so far
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(args.steps)]
+    # one HIP event pair on the launch stream around the K timed steps (a
+    # timing event pair per step put ~11 us of marker packets between the
+    # steps of a 0.14 ms configs[1] solve: tools/host_probe.py)
+    evs = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
+    evs[0].record(stream)
     for k in range(args.steps):
-        step(evs[k])
+        step()
+    evs[1].record(stream)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
-    # solve time on the launch stream (HIP events around hmpc_solve_batch:
-    # the solve kernel + the overflow pass)
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    # solve time per step on the launch stream (hmpc_solve_batch: classify,
+    # the class kernels, the overflow pass), averaged over the timed steps
+    kern_ms = evs[0].elapsed_time(evs[1]) / args.steps
     tt = torch.tensor([el, kern_ms], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -398,6 +398,7 @@ def main():
                                      '(SURVEY 0.3 / 8d); the frac is reported, not targeted',
                          'traffic_over_algorithmic': traffic / (bpsolve * B) if traffic else None,
                          'kernel': kernel, 'kernel_ms': kern_ms, 'kernel_ms_max_rank': kern_ms_max,
+                         'kernel_ms_basis': 'HIP events on the launch stream around the timed steps, / steps',
                          'algorithmic_bytes_per_solve': bpsolve, 'solves_per_launch': B,
                          'traffic_note': 'HBM bytes per launch from profiles/traffic.json (rocprofv3 '
                                          'FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md), null '

@@ -450,29 +450,35 @@ bool capturing(hipStream_t s) {
   return hipStreamIsCapturing(s, &st) == hipSuccess && st != hipStreamCaptureStatusNone;
 }
 
-// Before work on stream s: when the context's last solve went to another
+// Before work on stream s: when the context's last eager call went to another
 // stream, s waits for it (the context's workspaces and counters are shared by
-// every stream).  After: the solve's completion event, on s.  Skipped while s
-// captures: a wait on an event recorded outside the capture is not a graph
-// edge, and an event recorded inside it is never re-recorded by a replay, so
-// a later eager call would wait on a captured record.
+// every stream).  The completion event is recorded on that stream here, at
+// the switch -- it then covers everything enqueued there so far, the call
+// included -- not after every call: an event record per solve is a marker
+// packet between consecutive solves on one stream, 4 us of a 0.13 ms
+// configs[1] step.  So the last call's stream must stay valid
+// until the context's next call (include/hmpc.h).  Skipped while s captures:
+// a wait on an event recorded outside the capture is not a graph edge, and
+// mark_stream does not remember a capturing stream.
 int order_stream(hmpc_ctx* c, hipStream_t s) {
   if (capturing(s)) return HMPC_OK;
   if (c->has_last && c->last_stream != s) {
-    hipError_t e = hipStreamWaitEvent(s, c->last_ev, 0);
-    if (e != hipSuccess) return fail_hip(c, e, "hipStreamWaitEvent(last solve of this context)");
+    if (!c->last_ev) {
+      hipError_t e = hipEventCreateWithFlags(&c->last_ev, hipEventDisableTiming);
+      if (e != hipSuccess) return fail_hip(c, e, "hipEventCreate");
+    }
+    hipError_t e = hipEventRecord(c->last_ev, c->last_stream);
+    if (e != hipSuccess) return fail_hip(c, e, "hipEventRecord(last call's stream)");
+    e = hipStreamWaitEvent(s, c->last_ev, 0);
+    if (e != hipSuccess) return fail_hip(c, e, "hipStreamWaitEvent(last call of this context)");
   }
   return HMPC_OK;
 }
 
+// After work on stream s: remember it (eager calls only; a replay of a
+// captured call runs whenever the caller launches it)
 int mark_stream(hmpc_ctx* c, hipStream_t s) {
-  if (capturing(s)) return HMPC_OK;   // last_ev keeps the last eager solve
-  if (!c->last_ev) {
-    hipError_t e = hipEventCreateWithFlags(&c->last_ev, hipEventDisableTiming);
-    if (e != hipSuccess) return fail_hip(c, e, "hipEventCreate");
-  }
-  hipError_t e = hipEventRecord(c->last_ev, s);
-  if (e != hipSuccess) return fail_hip(c, e, "hipEventRecord(solve done)");
+  if (capturing(s)) return HMPC_OK;
   c->last_stream = s;
   c->has_last = true;
   return HMPC_OK;
@@ -504,7 +510,7 @@ int check_solve_args(hmpc_ctx* c, int64_t B, const void* x_in, const void* x_lin
 
 extern "C" {
 
-int hmpc_version(void) { return 10501; }
+int hmpc_version(void) { return 10502; }
 
 int hmpc_supported_horizons(int variant, int* Ns, int cap) {
   return hmpc::supported_horizons(variant, Ns, cap);
@@ -559,7 +565,7 @@ int hmpc_overflow_total(hmpc_ctx* c, int64_t* total) {
   if (!c || !total) return HMPC_ERR_ARG;
   *total = 0;
   if (!c->ovf_total) return HMPC_OK;   // no solve with an overflow pass yet
-  if (c->has_last) HMPC_HIP(c, hipEventSynchronize(c->last_ev));
+  if (c->has_last) HMPC_HIP(c, hipStreamSynchronize(c->last_stream));
   unsigned long long v = 0;
   HMPC_HIP(c, hipMemcpy(&v, c->ovf_total, sizeof v, hipMemcpyDeviceToHost));
   *total = (int64_t)v;

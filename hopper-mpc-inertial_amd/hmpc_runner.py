@@ -222,4 +222,7 @@ class Runner:
 def torch_from(a, like):
     """numpy array -> tensor on `like`'s device."""
     import torch
-    return torch.from_numpy(np.ascontiguousarray(a)).to(like.device)
+    a = np.ascontiguousarray(a)
+    if not a.flags.writeable:   # e.g. a broadcast view (torch wants a writable buffer)
+        a = a.copy()
+    return torch.from_numpy(a).to(like.device)

@@ -101,7 +101,9 @@ typedef struct hmpc_ctx hmpc_ctx;
    1.4.0 = + hmpc_set_order;
    1.5.0 = + hmpc_overflow_total;
    1.5.1 = hmpc_kernel_name / hmpc_active_capacity report the last solve's N = 60
-           kernel (capacity 64 at small batches) */
+           kernel (capacity 64 at small batches);
+   1.5.2 = the cross-stream completion event is recorded at a stream switch,
+           not after every call (the last call's stream must stay valid) */
 int hmpc_version(void);
 
 /* Which horizons have a dedicated (one- or two-wavefront) kernel for
@@ -113,8 +115,10 @@ int hmpc_version(void);
    outgrows its kernel's capacity in an overflow pass (capacity 6N).  The
    context's workspaces and counters are shared by its calls, so the context
    orders them itself: a call on a different stream than the context's last
-   one first makes its stream wait for that call's completion event
-   (hipStreamWaitEvent).  Eager calls on one context never overlap; use one
+   one first records an event on that last stream and makes its own stream
+   wait for it (hipStreamWaitEvent), so the stream of a context's last call
+   must stay valid until the context's next call (or hmpc_overflow_total,
+   which synchronises it).  Eager calls on one context never overlap; use one
    context per stream for concurrent solves.  Calls enqueued while their stream
    captures a HIP graph are outside this ordering (a replay runs whenever the
    caller launches it): the caller orders a graph's replays against the

@@ -34,7 +34,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_version_and_horizons():
     lib = hmpc.load()
-    assert lib.hmpc_version() == 10501   # 1.5.1: N = 60 names the last solve's kernel; 1.5: + hmpc_overflow_total; 1.4: + hmpc_set_order (1.3: stats, refinement; 1.2: planner, CasADi, precisions 4-5, capacity)
+    assert lib.hmpc_version() == 10502   # 1.5.2: completion event at a stream switch; 1.5.1: N = 60 names the last solve's kernel; 1.5: + hmpc_overflow_total; 1.4: + hmpc_set_order (1.3: stats, refinement; 1.2: planner, CasADi, precisions 4-5, capacity)
     hs = hmpc.supported_horizons('3f')
     assert 10 in hs and 20 in hs
     assert hmpc.supported_horizons('2f') == hs
