@@ -1466,28 +1466,77 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
     const double qr = qdiag(lane);
     const double ub_alias = (cc[N - 1] != 0.0) ? 2.0 * a.m * a.g : 0.0;
     double objl = 0.0;
-    for (int k = 0; k < N; ++k) {
-      const double cp = cs[2 * k], sp = cs[2 * k + 1];
-      const double* uk = vv + 6 * k;
-      const double u0 = uk[0], u1 = uk[1], u2 = uk[2], u3 = uk[3], u4 = uk[4], u5 = uk[5];
-      double nx = ad_lane(xr, dt, cp, sp, lane) + ((lane == 8) ? -a.g * dt : 0.0);
-      if (lane >= 6 && lane < 9) {
-        const int r = lane - 6;
-        nx += bv<VAR>(r, 0, dtm, cp, sp) * u0 + bv<VAR>(r, 1, dtm, cp, sp) * u1 + bv<VAR>(r, 2, dtm, cp, sp) * u2;
-      } else if (lane >= 9 && lane < 12) {
-        const double* bwr = bw + 18 * k + 6 * (lane - 9);
-        nx += ((bwr[0] * u0 + bwr[1] * u1) + (bwr[2] * u2 + bwr[3] * u3)) + (bwr[4] * u4 + bwr[5] * u5);
+    // the one-wave kernels: every lane loads its stage inputs (no divergent
+    // loads): lanes 9-11 their row of the omega block, lanes < 12 their x_ref
+    // entry, lanes < 6 their input; stage k+1's loads are issued before stage
+    // k's x store, which the compiler cannot move them across (one LDS round
+    // trip per stage on the rollout's chain otherwise).  The two-wave kernels,
+    // at their register cap, keep the plain loop (56 vs 24 B/lane of scratch).
+    if constexpr (RING == 3) {
+      const int rw = (lane >= 9 && lane < 12) ? lane - 9 : 0;
+      const int l12 = lane < 12 ? lane : 0, l6 = lane < 6 ? lane : 0;
+      struct Stage { double cp, sp, u[6], bwr[6], xr, ul, cck; };
+      auto load_stage = [&](int k, Stage& s) __attribute__((always_inline)) {
+        s.cp = cs[2 * k];
+        s.sp = cs[2 * k + 1];
+#pragma unroll
+        for (int c = 0; c < 6; ++c) s.u[c] = vv[6 * k + c];
+#pragma unroll
+        for (int c = 0; c < 6; ++c) s.bwr[c] = bw[18 * k + 6 * rw + c];
+        s.xr = un[12 * k + l12];
+        s.ul = vv[6 * k + l6];
+        s.cck = cc[k];
+      };
+      Stage cur, nxt;
+      load_stage(0, cur);
+      for (int k = 0; k < N; ++k) {
+        load_stage(k + 1 < N ? k + 1 : k, nxt);
+        const double cp = cur.cp, sp = cur.sp;
+        const double u0 = cur.u[0], u1 = cur.u[1], u2 = cur.u[2], u3 = cur.u[3], u4 = cur.u[4], u5 = cur.u[5];
+        double nx = ad_lane(xr, dt, cp, sp, lane) + ((lane == 8) ? -a.g * dt : 0.0);
+        if (lane >= 6 && lane < 9) {
+          const int r = lane - 6;
+          nx += bv<VAR>(r, 0, dtm, cp, sp) * u0 + bv<VAR>(r, 1, dtm, cp, sp) * u1 + bv<VAR>(r, 2, dtm, cp, sp) * u2;
+        } else if (lane >= 9 && lane < 12) {
+          const double* bwr = cur.bwr;
+          nx += ((bwr[0] * u0 + bwr[1] * u1) + (bwr[2] * u2 + bwr[3] * u3)) + (bwr[4] * u4 + bwr[5] * u5);
+        }
+        xr = lane < 12 ? nx : 0.0;
+        const double kf = (k == N - 1) ? kTermQ : 1.0;
+        const double e = lane < 12 ? xr - cur.xr : 0.0;
+        objl = fma(kf * qr * e, e, objl);
+        if (k < N - 1 && lane < 6) {
+          const double ub = a.uref_aliased ? ub_alias : ((cur.cck != 0.0) ? 2.0 * a.m * a.g : 0.0);
+          const double du = cur.ul - (lane == 2 ? ub : 0.0);
+          objl = fma(kRdiag * du, du, objl);
+        }
+        if (lane < 12) xo[12 * (k + 1) + lane] = xr;
+        cur = nxt;
       }
-      xr = lane < 12 ? nx : 0.0;
-      const double kf = (k == N - 1) ? kTermQ : 1.0;
-      const double e = lane < 12 ? xr - un[12 * k + lane] : 0.0;
-      objl = fma(kf * qr * e, e, objl);
-      if (k < N - 1 && lane < 6) {
-        const double ub = a.uref_aliased ? ub_alias : ((cc[k] != 0.0) ? 2.0 * a.m * a.g : 0.0);
-        const double du = uk[lane] - (lane == 2 ? ub : 0.0);
-        objl = fma(kRdiag * du, du, objl);
+    } else {
+      for (int k = 0; k < N; ++k) {
+        const double cp = cs[2 * k], sp = cs[2 * k + 1];
+        const double* uk = vv + 6 * k;
+        const double u0 = uk[0], u1 = uk[1], u2 = uk[2], u3 = uk[3], u4 = uk[4], u5 = uk[5];
+        double nx = ad_lane(xr, dt, cp, sp, lane) + ((lane == 8) ? -a.g * dt : 0.0);
+        if (lane >= 6 && lane < 9) {
+          const int r = lane - 6;
+          nx += bv<VAR>(r, 0, dtm, cp, sp) * u0 + bv<VAR>(r, 1, dtm, cp, sp) * u1 + bv<VAR>(r, 2, dtm, cp, sp) * u2;
+        } else if (lane >= 9 && lane < 12) {
+          const double* bwr = bw + 18 * k + 6 * (lane - 9);
+          nx += ((bwr[0] * u0 + bwr[1] * u1) + (bwr[2] * u2 + bwr[3] * u3)) + (bwr[4] * u4 + bwr[5] * u5);
+        }
+        xr = lane < 12 ? nx : 0.0;
+        const double kf = (k == N - 1) ? kTermQ : 1.0;
+        const double e = lane < 12 ? xr - un[12 * k + lane] : 0.0;
+        objl = fma(kf * qr * e, e, objl);
+        if (k < N - 1 && lane < 6) {
+          const double ub = a.uref_aliased ? ub_alias : ((cc[k] != 0.0) ? 2.0 * a.m * a.g : 0.0);
+          const double du = uk[lane] - (lane == 2 ? ub : 0.0);
+          objl = fma(kRdiag * du, du, objl);
+        }
+        if (lane < 12) xo[12 * (k + 1) + lane] = xr;
       }
-      if (lane < 12) xo[12 * (k + 1) + lane] = xr;
     }
     const double objv = wave_sum(objl);
     wsync();
