@@ -54,17 +54,20 @@ def _inputs(start, count, dev, n=N, curve=True):
             for k in ('x_in', 'x_lin', 'x_ref', 'pf', 'C', 'mu')}
 
 
-def _worker(rank, world, port, q, wl):
+def _worker(rank, world, port, q, wl, backend='gloo'):
     import sys
     for p in (os.path.join(ROOT, 'hopper-mpc-inertial_amd'), ROOT):
         sys.path.insert(0, p)
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
-    dist.init_process_group('gloo', rank=rank, world_size=world)
-    import hmpc
-    import hmpc_dist
     dev = torch.device('cuda', 0)
     torch.cuda.set_device(dev)
+    if backend == 'nccl':
+        dist.init_process_group('nccl', rank=rank, world_size=world, device_id=dev)
+    else:
+        dist.init_process_group('gloo', rank=rank, world_size=world)
+    import hmpc
+    import hmpc_dist
     n, curve, gb, kernel = WORKLOADS[wl]
     if gb:   # strong split of a fixed global batch (bench.py --global-batch)
         start, cnt = hmpc_dist.strong_shard(gb, world, rank)
@@ -85,7 +88,8 @@ def _worker(rank, world, port, q, wl):
     ex.wait()
     torch.cuda.synchronize(dev)
     oa, sa = ex.results(slot)
-    q.put((rank, oa.cpu().numpy().copy(), sa.cpu().numpy().copy(), start, u.cpu().numpy().copy()))
+    q.put((rank, oa.cpu().numpy().copy(), sa.cpu().numpy().copy(), start, u.cpu().numpy().copy(),
+           dict(ex.calls), dist.get_backend()))
     dist.barrier()
     ctx.close()
     dist.destroy_process_group()
@@ -118,8 +122,36 @@ def test_pipelined_exchange_equals_single_process(wl):
     u_ref = out['u'].cpu().numpy()
     ctx1.close()
     assert (st_ref == 0).mean() > 0.9
-    for _, oa, sa, start, u in res:
+    for _, oa, sa, start, u, calls, backend in res:
+        assert backend == 'gloo' and calls['all_gather_list'] == STEPS, calls
         assert np.array_equal(sa, st_ref)
         assert np.array_equal(oa, obj_ref)   # bitwise: shards are batch-position invariant
         assert np.array_equal(u, u_ref[start:start + len(u)])
     assert sorted(r[3] for r in res)[1] == len(min(res, key=lambda r: r[3])[4])   # shards tile
+
+
+def test_rccl_exchange_one_rank():
+    """The exchange's RCCL branch on hardware: one rank on the nccl (= RCCL)
+    backend, so ResultExchange takes all_gather_into_tensor on its side
+    stream (a one-GPU box cannot hold two RCCL ranks; the 2/4/8-rank
+    collective is the driver's SCALE run).  The gathered objectives and
+    statuses equal a plain solve of the same batch bit for bit."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    p = ctx.Process(target=_worker, args=(0, 1, _free_port(), q, 'cfg2_weak', 'nccl'))
+    p.start()
+    _, oa, sa, start, u, calls, backend = q.get(timeout=240)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    assert backend == 'nccl'
+    assert calls == {'all_gather_into_tensor': STEPS, 'all_gather_list': 0}, calls
+    import hmpc
+    d = _inputs(0, PER_RANK, torch.device('cuda', 0), N, True)
+    ctx1 = _ctx(hmpc, N)
+    out = ctx1.solve_device(d['x_in'], d['x_lin'], d['x_ref'], d['pf'], d['C'], mu=d['mu'])
+    torch.cuda.synchronize()
+    assert np.array_equal(sa, out['status'].cpu().numpy())
+    assert np.array_equal(oa, out['obj'].cpu().numpy())
+    assert np.array_equal(u, out['u'].cpu().numpy())
+    ctx1.close()
