@@ -1486,6 +1486,8 @@ solve_kernel(SolveArgs a) {
 #pragma unroll 1
       for (int pass = 0; pass < 2 && qu > 0; ++pass) {
         if constexpr (W == 1) {   // modified Gram-Schmidt: no barriers in one wave
+          // (a classical form in blocks of four independent sums measured
+          // -0.3 % at configs[2], no gain at configs[1]: DESIGN.md 7)
           ladder<0, QMAX>(qu, [&](auto lc) __attribute__((always_inline)) {
             constexpr int l = decltype(lc)::value;
             const real cl = B::sum(Qw[l] * wp, red);
@@ -1526,9 +1528,15 @@ solve_kernel(SolveArgs a) {
       real rcur = tid < qu ? cbv[tid] : 0.0, rmine = 0.0;
       const int td = tid < qu ? tid : 0;
       const real rinv = real(1) / Rm[loff(td) + td];
+      // each step's R column is loaded one step ahead (its LDS latency off
+      // the readlane -> mul -> fma chain)
+      const int lt = qu > 0 ? qu - 1 : 0;
+      real rv_n = Rm[loff(lt) + (tid < lt ? tid : 0)];
       for (int l = qu - 1; l >= 0; --l) {
+        const real rv = rv_n;
+        const int ln = l > 0 ? l - 1 : 0;
+        rv_n = Rm[loff(ln) + (tid < ln ? tid : 0)];
         const real rl = B::bcast(rcur, l, red) * B::bcast(rinv, l, red);
-        const real rv = Rm[loff(l) + (tid < l ? tid : 0)];
         rmine = (tid == l) ? rl : rmine;
         rcur = (tid < l) ? fma(-rv, rl, rcur) : rcur;
       }
