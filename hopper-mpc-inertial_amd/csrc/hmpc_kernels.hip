@@ -998,12 +998,42 @@ solve_kernel(SolveArgs a) {
       const unsigned dumpa = lds_addr(sm + L::COLB + tid);
       xs[tid] = 0.0;
       B::sync();   // every lane's S / adjoint reads are issued before the first H store
+      real cp_up = 0.0, sp_up = 0.0;   // cos / sin of the stage above (advance)
       sfor<0, N>([&](auto jc) __attribute__((always_inline)) {
         constexpr int j = N - 1 - decltype(jc)::value;
-        const real* smj = sm + opaque_zero();   // keeps this step's loads here
-        advance(std::integral_constant<int, j>{}, smj);
-        const real cp = smj[L::CS + 2 * j], sp = smj[L::CS + 2 * j + 1];
-        const real* bw = smj + L::BW + 18 * j;
+        // stage j's rows 9..11 of Bd and cos / sin in one LDS round trip (ten
+        // broadcast loads, one wait): the compiler otherwise sinks each load
+        // next to its product and waits for it there, three round trips per
+        // entry of H in series
+        real2 bwp[9], csp;
+        {
+          const unsigned sb = lds_addr(sm + opaque_zero());
+          sfor<0, 9>([&](auto ic) __attribute__((always_inline)) {
+            constexpr int i = decltype(ic)::value;
+            lds_ld2<RB * (L::BW + 18 * j + 2 * i)>(bwp[i], sb);
+          });
+          lds_ld2<RB * (L::CS + 2 * j)>(csp, sb);
+          lds_wait<0>(bwp[0], bwp[1], bwp[2], bwp[3]);
+          lds_wait<0>(bwp[4], bwp[5], bwp[6], bwp[7]);
+          lds_wait<0>(bwp[8], csp);
+        }
+        real bw[18];
+#pragma unroll
+        for (int i = 0; i < 9; ++i) {
+          bw[2 * i] = bwp[i].x;
+          bw[2 * i + 1] = bwp[i].y;
+        }
+        if constexpr (j < N - 1) {   // g -> g_j = Ad_{j+1}' g_{j+1} (as advance())
+          real gn[12];
+#pragma unroll
+          for (int r = 0; r < 12; ++r) gn[r] = g[r];
+          adt_times(gn, dt, cp_up, sp_up);
+#pragma unroll
+          for (int r = 0; r < 12; ++r) g[r] = (ii > j) ? gn[r] : g[r];
+        }
+        const real cp = csp.x, sp = csp.y;
+        cp_up = cp;
+        sp_up = sp;
         const bool st = (smask >> j) & 1;   // uniform
         const int o = stage_off(j);
         auto put = [&](int w, real val) __attribute__((always_inline)) {
