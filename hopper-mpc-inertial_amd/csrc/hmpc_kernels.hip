@@ -1993,8 +1993,8 @@ solve_kernel(SolveArgs a) {
       xr = ad_lane(xr, dt, cp, sp) + bu + gdt;
       xk[k] = xr;
       if constexpr (k < N - 1) {
-        const real ub = a.uref_aliased ? ((sm[L::CC + N - 1] != 0.0) ? 2.0 * a.m * a.g : 0.0)
-                                         : ((sm[L::CC + k] != 0.0) ? 2.0 * a.m * a.g : 0.0);
+        // (C[k] != 0 is bit k of smask: no LDS round trip inside the rollout)
+        const real ub = ((smask >> (a.uref_aliased ? N - 1 : k)) & 1) ? 2.0 * a.m * a.g : 0.0;
         const real du = fma(-ubz, ub, uk[tu]);
         objl = fma(rdu * du, du, objl);
       }

@@ -606,11 +606,26 @@ __global__ void __launch_bounds__(64, HMPC_SWING_WAVES) swing_kernel(SolveArgs a
     // Ad' leaves the angle rows (f3, f4, f5) alone and adds dt Rz' of them to
     // the rate rows.  Entries right of the diagonal (j > i) keep the finite
     // values that fall out; only the lower triangle is read.
+    double cp_up = 0.0, sp_up = 0.0;   // cos / sin of the stage above
     sfor<0, N>([&](auto jc) __attribute__((always_inline)) {
       constexpr int j = N - 1 - decltype(jc)::value;
-      const double* smj = sm + opaque_zero();   // keeps this step's loads here
+      // stage j's torque block of Bd and cos / sin in one LDS round trip
+      // (eleven loads, one wait) instead of one per product
+      double bw[9], cj, sj;
+      {
+        const unsigned sb = lds_addr(sm + opaque_zero());
+        sfor<0, 9>([&](auto ic) __attribute__((always_inline)) {
+          constexpr int i = decltype(ic)::value;
+          lds_ld1o<8 * (L::BW + 9 * j + i)>(bw[i], sb);
+        });
+        lds_ld1o<8 * (L::CS + 2 * j)>(cj, sb);
+        lds_ld1o<8 * (L::CS + 2 * j + 1)>(sj, sb);
+        sfor<0, 9>([&](auto ic) __attribute__((always_inline)) { lds_wait<0>(bw[decltype(ic)::value]); });
+        lds_wait<0>(cj);
+        lds_wait<0>(sj);
+      }
       if constexpr (j < N - 1) {
-        const double cp1 = smj[L::CS + 2 * (j + 1)], sp1 = smj[L::CS + 2 * (j + 1) + 1];
+        const double cp1 = cp_up, sp1 = sp_up;
         const double n9 = g9 + ((cp1 * dt) * f3 + (-sp1 * dt) * f4);
         const double n10 = g10 + ((sp1 * dt) * f3 + (cp1 * dt) * f4);
         const double n11 = fma(dt, f5, g11);
@@ -618,7 +633,8 @@ __global__ void __launch_bounds__(64, HMPC_SWING_WAVES) swing_kernel(SolveArgs a
         g10 = (ii > j) ? n10 : g10;
         g11 = (ii > j) ? n11 : g11;
       }
-      const double* bw = smj + L::BW + 9 * j;
+      cp_up = cj;
+      sp_up = sj;
       sfor<0, 3>([&](auto cc) __attribute__((always_inline)) {
         constexpr int c2 = decltype(cc)::value;
         double acc = 0.0;
