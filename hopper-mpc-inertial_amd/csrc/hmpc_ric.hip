@@ -903,13 +903,18 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
   // ---------------- phase 3: unconstrained optimum v0 = -H^-1 h --------------
   hinv(vv, N - 1);
   // |n| of the z rows (lane k): zc sqrt(sum_{j <= k-2, stance} (k-1-j)^2)
-  if (lane < N) {
-    double s2 = 0.0;
-    for (int j = 0; j + 2 <= lane; ++j) {
-      const double cz = (double)(lane - 1 - j);
-      if (cc[j] != 0.0) s2 = fma(cz, cz, s2);
+  {
+    // the stance stages as one wave-uniform mask (N <= 64): the loop reads no
+    // LDS, where one dependent load per stage cost a round trip each
+    const uint64_t stm = __ballot(lane < N && cc[lane < N ? lane : 0] != 0.0);
+    if (lane < N) {
+      double s2 = 0.0;
+      for (int j = 0; j + 2 <= lane; ++j) {
+        const double cz = (double)(lane - 1 - j);
+        if ((stm >> j) & 1) s2 = fma(cz, cz, s2);
+      }
+      znrm[lane] = zc * sqrt(s2);
     }
-    znrm[lane] = zc * sqrt(s2);
   }
   wsync();
 
