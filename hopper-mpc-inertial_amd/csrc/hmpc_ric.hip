@@ -283,36 +283,95 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
     double xr = lane < 12 ? xin[lane] : 0.0;
     const double qr = qdiag(lane);
     if (lane == 2) zb[0] = xr;
-    for (int k = 0; k < N; ++k) {
-      xr = ad_lane(xr, dt, cs[2 * k], cs[2 * k + 1], lane) + ((lane == 8) ? -a.g * dt : 0.0);
-      const double kf = (k == N - 1) ? kTermQ : 1.0;
-      if (lane < 12) dd[12 * k + lane] = kf * qr * (xr - un[12 * k + lane]);
-      if (lane == 2) zb[k + 1] = xr;
-    }
-    wsync();
     const double ubar_alias = (cc[N - 1] != 0.0) ? 2.0 * a.m * a.g : 0.0;
-    double ar = lane < 12 ? dd[12 * (N - 1) + lane] : 0.0;   // a_N = d_N
-    for (int t = N; t >= 1; --t) {
-      const int i = t - 1;
-      const double a6 = rdlane(ar, 6), a7 = rdlane(ar, 7), a8 = rdlane(ar, 8);
-      const double a9 = rdlane(ar, 9), a10 = rdlane(ar, 10), a11 = rdlane(ar, 11);
-      {   // lanes c < 6 (branch-free; the others compute a copy of input 0)
-        const int c = lane < 6 ? lane : 0;
-        const double cp = cs[2 * i], sp = cs[2 * i + 1];
-        const double* bwi = bw + 18 * i;
-        double acc = bwi[c] * a9 + bwi[6 + c] * a10 + bwi[12 + c] * a11;
-        const double af = bv<VAR>(0, c, dtm, cp, sp) * a6 + bv<VAR>(1, c, dtm, cp, sp) * a7 +
-                          bv<VAR>(2, c, dtm, cp, sp) * a8;
-        acc = c < 3 ? acc + af : acc;
-        const bool stance = cc[i] != 0.0;
-        const bool fr = c >= 3 || (stance && !(VAR == 2 && c == 1));
-        const double ub = a.uref_aliased ? ubar_alias : (stance ? 2.0 * a.m * a.g : 0.0);
-        const double hz = 2.0 * acc - 2.0 * kRdiag * ub;
-        const double h = fr ? ((c == 2 && i < N - 1) ? hz : 2.0 * acc) : 0.0;
-        if (lane < 6) nb[6 * i + c] = -h;
+    if constexpr (ENT == 1) {
+      // both recursions load each stage's data one iteration ahead (x_ref,
+      // cos / sin, Bd rows, C, d_t do not depend on the carried state): the
+      // loads of the next iteration are in flight while this one's chain
+      // runs, instead of a round trip in series at the head of every
+      // iteration.  (Main kernels only: in the overflow kernel this form
+      // put an AGPR copy before an EXEC restore, tests/test_exec_lint.py.)
+      const int l12 = lane < 12 ? lane : 0;
+      double cpn = cs[0], spn = cs[1], unn = un[l12];
+      for (int k = 0; k < N; ++k) {
+        const double cpk = cpn, spk = spn, uk = unn;
+        const int k1 = k + 1 < N ? k + 1 : k;
+        cpn = cs[2 * k1];
+        spn = cs[2 * k1 + 1];
+        unn = un[12 * k1 + l12];
+        xr = ad_lane(xr, dt, cpk, spk, lane) + ((lane == 8) ? -a.g * dt : 0.0);
+        const double kf = (k == N - 1) ? kTermQ : 1.0;
+        if (lane < 12) dd[12 * k + lane] = kf * qr * (xr - uk);
+        if (lane == 2) zb[k + 1] = xr;
       }
-      if (t >= 2) {
-        ar = adt_lane(ar, dt, cs[2 * i], cs[2 * i + 1], lane) + (lane < 12 ? dd[12 * (t - 2) + lane] : 0.0);
+      wsync();
+      double ar = lane < 12 ? dd[12 * (N - 1) + lane] : 0.0;   // a_N = d_N
+      const int c6 = lane < 6 ? lane : 0;
+      struct StageB { double cp, sp, b0, b1, b2, st, d; };
+      auto load_stage = [&](int i, StageB& s) __attribute__((always_inline)) {
+        s.cp = cs[2 * i];
+        s.sp = cs[2 * i + 1];
+        s.b0 = bw[18 * i + c6];
+        s.b1 = bw[18 * i + 6 + c6];
+        s.b2 = bw[18 * i + 12 + c6];
+        s.st = cc[i];
+        s.d = dd[12 * (i >= 1 ? i - 1 : 0) + l12];   // d_{t-1} of the a update (t >= 2)
+      };
+      StageB nx;
+      load_stage(N - 1, nx);
+      for (int t = N; t >= 1; --t) {
+        const int i = t - 1;
+        const StageB cur = nx;
+        load_stage(i >= 1 ? i - 1 : 0, nx);
+        const double a6 = rdlane(ar, 6), a7 = rdlane(ar, 7), a8 = rdlane(ar, 8);
+        const double a9 = rdlane(ar, 9), a10 = rdlane(ar, 10), a11 = rdlane(ar, 11);
+        {   // lanes c < 6 (branch-free; the others compute a copy of input 0)
+          const int c = c6;
+          const double cp = cur.cp, sp = cur.sp;
+          double acc = cur.b0 * a9 + cur.b1 * a10 + cur.b2 * a11;
+          const double af = bv<VAR>(0, c, dtm, cp, sp) * a6 + bv<VAR>(1, c, dtm, cp, sp) * a7 +
+                            bv<VAR>(2, c, dtm, cp, sp) * a8;
+          acc = c < 3 ? acc + af : acc;
+          const bool stance = cur.st != 0.0;
+          const bool fr = c >= 3 || (stance && !(VAR == 2 && c == 1));
+          const double ub = a.uref_aliased ? ubar_alias : (stance ? 2.0 * a.m * a.g : 0.0);
+          const double hz = 2.0 * acc - 2.0 * kRdiag * ub;
+          const double h = fr ? ((c == 2 && i < N - 1) ? hz : 2.0 * acc) : 0.0;
+          if (lane < 6) nb[6 * i + c] = -h;
+        }
+        if (t >= 2) ar = adt_lane(ar, dt, cur.cp, cur.sp, lane) + (lane < 12 ? cur.d : 0.0);
+      }
+    } else {
+      for (int k = 0; k < N; ++k) {
+        xr = ad_lane(xr, dt, cs[2 * k], cs[2 * k + 1], lane) + ((lane == 8) ? -a.g * dt : 0.0);
+        const double kf = (k == N - 1) ? kTermQ : 1.0;
+        if (lane < 12) dd[12 * k + lane] = kf * qr * (xr - un[12 * k + lane]);
+        if (lane == 2) zb[k + 1] = xr;
+      }
+      wsync();
+      double ar = lane < 12 ? dd[12 * (N - 1) + lane] : 0.0;   // a_N = d_N
+      for (int t = N; t >= 1; --t) {
+        const int i = t - 1;
+        const double a6 = rdlane(ar, 6), a7 = rdlane(ar, 7), a8 = rdlane(ar, 8);
+        const double a9 = rdlane(ar, 9), a10 = rdlane(ar, 10), a11 = rdlane(ar, 11);
+        {   // lanes c < 6 (branch-free; the others compute a copy of input 0)
+          const int c = lane < 6 ? lane : 0;
+          const double cp = cs[2 * i], sp = cs[2 * i + 1];
+          const double* bwi = bw + 18 * i;
+          double acc = bwi[c] * a9 + bwi[6 + c] * a10 + bwi[12 + c] * a11;
+          const double af = bv<VAR>(0, c, dtm, cp, sp) * a6 + bv<VAR>(1, c, dtm, cp, sp) * a7 +
+                            bv<VAR>(2, c, dtm, cp, sp) * a8;
+          acc = c < 3 ? acc + af : acc;
+          const bool stance = cc[i] != 0.0;
+          const bool fr = c >= 3 || (stance && !(VAR == 2 && c == 1));
+          const double ub = a.uref_aliased ? ubar_alias : (stance ? 2.0 * a.m * a.g : 0.0);
+          const double hz = 2.0 * acc - 2.0 * kRdiag * ub;
+          const double h = fr ? ((c == 2 && i < N - 1) ? hz : 2.0 * acc) : 0.0;
+          if (lane < 6) nb[6 * i + c] = -h;
+        }
+        if (t >= 2) {
+          ar = adt_lane(ar, dt, cs[2 * i], cs[2 * i + 1], lane) + (lane < 12 ? dd[12 * (t - 2) + lane] : 0.0);
+        }
       }
     }
   }
