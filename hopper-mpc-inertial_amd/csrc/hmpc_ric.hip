@@ -951,8 +951,11 @@ __device__ void ric_solve(const SolveArgs& a, const int N_, const int64_t b, dou
   };
   // lane k: sum_{j <= k-2} zc (k-1-j) C_j X[fz_j] (the z-row of stage k over
   // X) = zc * (exclusive scan of the exclusive scan of C_j X[fz_j])
+  // (the lane's stance flag once, not an LDS load ahead of X's in every call)
+  const bool zst = lane < N && cc[lane < N ? lane : 0] != 0.0;
   auto zdot = [&](const double* X) -> double {
-    const double aj = (lane < N && cc[lane < N ? lane : 0] != 0.0) ? X[6 * (lane < N ? lane : 0) + 2] : 0.0;
+    const double xz = X[6 * (lane < N ? lane : 0) + 2];
+    const double aj = zst ? xz : 0.0;
     const double e1 = wave_scan(aj) - aj;
     return zc * (wave_scan(e1) - e1);
   };
